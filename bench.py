@@ -1,0 +1,217 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X BERT/BGE embedding forward (BASELINE.json metric).
+
+One step = one forward of the workload's batch (bge-base-en-v1.5 architecture,
+q4_0 weights, 64 sentences x 512 tokens per GPU) through libbert.so's
+device-resident entry point (bertx_forward_device), with token ids already in HBM.
+Multi-GPU: one process per GPU (torchrun); every rank runs its own 64-sentence
+shard ("weak" scaling, no data-path collective -- the path is embarrassingly
+parallel); the timed region is bracketed by barriers and the max over ranks is
+reported.  Weights are synthetic (random init of the architecture, seeded) --
+there are no checkpoints offline.
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "embeddings.cpp_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+MFMA_F16_PEAK_TFLOPS = 2500.0    # MI355X dense f16/bf16 MFMA (MI355X_MICROARCH.md, chip table)
+HBM_PEAK_GBPS = 8000.0
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--arch", default="bge-base-en-v1.5")
+    p.add_argument("--ftype", default="q4_0")
+    p.add_argument("--batch", type=int, default=64, help="sentences per GPU")
+    p.add_argument("--seq", type=int, default=512)
+    p.add_argument("--seed", type=int, default=1234)
+    p.add_argument("--model-dir", default=os.environ.get("EMB_MODEL_DIR", "/tmp/emb_models"))
+    p.add_argument("--cpu-baseline-sentences", type=int, default=24)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-profile", action="store_true", help="disable live per-kernel event timing")
+    return p.parse_args()
+
+
+def dist_env():
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return rank, world, local
+
+
+def algorithmic_bytes(hp, ftype, B, L):
+    """Compulsory HBM bytes of one batch: weights at stored width,
+    f32 biases/LN, gathered embedding rows, ids in, embeddings out."""
+    bpw = {"f32": 4.0, "f16": 2.0, "q4_0": 0.5625, "q4_1": 0.625, "q8_0": 1.0625}[ftype]
+    d, f, nl = hp["n_embd"], hp["n_intermediate"], hp["n_layer"]
+    w = nl * (4 * d * d + 2 * d * f) * bpw
+    small = nl * (9 * d + f) * 4 + 4 * d * 4
+    emb_rows = B * L * d * bpw * 2 + 2 * d * bpw
+    return w + small + emb_rows + 4 * B * L + 4 * B * d
+
+
+def main():
+    a = parse()
+    rank, world, local = dist_env()
+    os.environ["BERT_DEVICES"] = str(local)
+    import numpy as np
+    import torch
+    import bertpy
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend)
+    else:
+        torch.cuda.set_device(local)
+
+    hp = bertpy.ARCHS[a.arch]
+    os.makedirs(a.model_dir, exist_ok=True)
+    path = os.path.join(a.model_dir, f"{a.arch}-{a.ftype}-seed{a.seed}.bin")
+    if rank == 0 and not os.path.exists(path):
+        bertpy.synthetic_model(path + ".part", a.arch, a.ftype, seed=a.seed)
+        os.replace(path + ".part", path)
+    if dist is not None:
+        dist.barrier()
+
+    lib = bertpy.load_lib()
+    model = bertpy.BertModel(path, lib=lib)
+    ctx = model.ctx
+    d = model.n_embd
+    B, L = a.batch, a.seq
+    ids_list = bertpy.synthetic_ids(B, L, hp["n_vocab"], seed=7 + rank)
+    dev = torch.device("cuda", local)
+    ids = torch.from_numpy(np.concatenate(ids_list).astype(np.int32)).to(dev)
+    cu = torch.arange(0, (B + 1) * L, L, dtype=torch.int32).to(dev)
+    out = torch.empty((B, d), dtype=torch.float32, device=dev)
+    T = B * L
+    assert lib.bertx_reserve(ctx, 0, T, B) == 0
+    stream = torch.cuda.current_stream(dev)
+    sp = ctypes.c_void_p(stream.cuda_stream)
+
+    def step():
+        rc = lib.bertx_forward_device(ctx, 0, ctypes.c_void_p(ids.data_ptr()), ctypes.c_void_p(cu.data_ptr()),
+                                      B, L, T, ctypes.c_void_p(out.data_ptr()), sp)
+        if rc != 0:
+            raise RuntimeError(f"bertx_forward_device failed: {rc}")
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    e = out.float().cpu().numpy()
+    assert np.all(np.isfinite(e)) and np.allclose(np.linalg.norm(e, axis=1), 1.0, atol=1e-3), "bad embeddings"
+
+    lib.bertx_set_profiling(ctx, 0 if a.no_profile else 1)
+    lib.bertx_reset_stats(ctx)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if dist is not None:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    lib.bertx_set_profiling(ctx, 0)
+    stats = model.kernel_stats()
+
+    ms_per_step = elapsed / a.steps * 1e3
+    value = B * world * a.steps / elapsed
+
+    roofline = None
+    kernels = {}
+    for s in stats:
+        if s["launches"]:
+            kernels[s["name"]] = {"launches": s["launches"], "avg_us": s["ms"] / s["launches"] * 1e3,
+                                  "share": 0.0}
+    tot_ms = sum(s["ms"] for s in stats) or 1.0
+    for s in stats:
+        if s["launches"]:
+            kernels[s["name"]]["share"] = round(s["ms"] / tot_ms, 4)
+    if stats and not a.no_profile:
+        dom = max(stats, key=lambda s: s["ms"])
+        if dom["launches"]:
+            avg_s = dom["ms"] / dom["launches"] * 1e-3
+            per_launch = dom["work"] / dom["launches"]
+            if dom["work_is_flops"]:
+                ach = per_launch / avg_s / 1e12
+                roofline = {"kernel": dom["name"], "bound": "mfma", "achieved": round(ach, 2),
+                            "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / MFMA_F16_PEAK_TFLOPS, 4),
+                            "work_per_launch": per_launch, "avg_launch_us": round(avg_s * 1e6, 2), "traffic": None}
+            else:
+                ach = per_launch / avg_s / 1e9
+                roofline = {"kernel": dom["name"], "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS,
+                            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None}
+        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if roofline and os.path.exists(pmc):
+            try:
+                with open(pmc) as f:
+                    tr = json.load(f).get(roofline["kernel"])
+                if tr is not None:
+                    roofline["traffic"] = tr
+            except Exception:
+                pass
+
+    alg_bytes = algorithmic_bytes(hp, a.ftype, B, L)
+    res = {
+        "metric": "sentences/sec + HBM GB/s, bge-base-en-v1.5 q4_0 seq512 batch64, 1/2/4/8 GPU",
+        "value": round(value, 2), "unit": "sentences/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f16", "data": "synthetic (random-init weights, seeded token ids)",
+        "config": {"workload": f"{a.arch} {a.ftype} seq_len {L}, {B} sentences per GPU (bert_forward_batch path)",
+                   "batch_per_gpu": B, "global_batch": B * world, "seq_len": L, "weights": a.ftype,
+                   "parallelism": f"replicas x{world} (no collectives)"},
+        "hbm_gbps_algorithmic": round(alg_bytes / (ms_per_step * 1e-3) / 1e9, 2),
+        "roofline": roofline,
+        "kernels": kernels,
+    }
+
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        try:
+            import oracle_lib
+            n_thr = min(16, os.cpu_count() or 1)
+            orc = oracle_lib.Oracle(path)
+            sample = [x for x in ids_list[: a.cpu_baseline_sentences]]
+            c0 = time.perf_counter()
+            emb_cpu = orc.forward_batch(sample, n_threads=n_thr)
+            c1 = time.perf_counter()
+            cos = float(np.min(np.sum(emb_cpu * e[: len(sample)], axis=1)))
+            res["cpu_baseline"] = {"value": round(len(sample) / (c1 - c0), 4), "unit": "sentences/s",
+                                   "cores": n_thr, "kind": "port",
+                                   "sample": f"{len(sample)} of the {B} sentences (L={L}) through the C oracle "
+                                             f"(oracle/bert_oracle.c, ggml-era q8 activation path), "
+                                             f"{c1 - c0:.1f} s",
+                                   "gpu_vs_cpu_min_cosine": round(cos, 6)}
+        except Exception as ex:  # the baseline is a report, never the product
+            res["cpu_baseline"] = {"value": None, "error": str(ex)}
+
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,286 @@
+"""Python host side of the MI355X embedding engine.
+
+* ``BertModel`` mirrors the reference's ctypes client (examples/sample_dylib.py:17-62:
+  same constructor argument, ``n_embd``, ``encode(sentences, batch_size=16)``) on top of
+  the C ABI of ``build/libbert.so`` -- the library does all the work (tokenizer, HIP
+  kernels, multi-GPU sharding); this module only marshals pointers.
+* ``load_lib`` declares argtypes for every symbol of include/bert.h and
+  include/bert_hip.h.
+* ``write_model`` / ``synthetic_model`` write model files in the reference's format
+  (reference bert.cpp:434-766, models/convert-to-ggml.py:68-108) so a GPU box with no
+  checkpoints can build the BASELINE architectures from a seed.
+"""
+import ctypes
+import os
+import struct
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+LIB_PATH = os.path.join(ROOT, "build", "libbert.so")
+
+FTYPE = {"f32": 0, "f16": 1, "q4_0": 2, "q4_1": 3, "q8_0": 8}
+
+_lib = None
+
+c_i32 = ctypes.c_int32
+c_f32p = ctypes.POINTER(ctypes.c_float)
+c_i32p = ctypes.POINTER(ctypes.c_int32)
+
+
+def load_lib(path=None):
+    """Load libbert.so once and declare its ABI.  Raises if the build is missing."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise RuntimeError(f"{p} not built: run `make -C embeddings.cpp_amd` (or __graft_entry__.build())")
+    L = ctypes.CDLL(p)
+    vp = ctypes.c_void_p
+    L.bert_load_from_file.restype = vp
+    L.bert_load_from_file.argtypes = [ctypes.c_char_p]
+    L.bert_free.argtypes = [vp]
+    L.bert_n_embd.restype = c_i32
+    L.bert_n_embd.argtypes = [vp]
+    L.bert_n_max_tokens.restype = c_i32
+    L.bert_n_max_tokens.argtypes = [vp]
+    L.bert_vocab_id_to_token.restype = ctypes.c_char_p
+    L.bert_vocab_id_to_token.argtypes = [vp, c_i32]
+    L.bert_tokenize.argtypes = [vp, ctypes.c_char_p, c_i32p, c_i32p, c_i32]
+    L.bert_encode.argtypes = [vp, c_i32, ctypes.c_char_p, c_f32p]
+    L.bert_encode_batch.argtypes = [vp, c_i32, c_i32, c_i32, ctypes.POINTER(ctypes.c_char_p),
+                                    ctypes.POINTER(c_f32p)]
+    L.bert_forward.argtypes = [vp, c_i32, c_i32p, c_i32, c_f32p]
+    for fn in (L.bert_forward_batch, L.bert_forward_fake_batch):
+        fn.argtypes = [vp, c_i32, c_i32, ctypes.POINTER(c_i32p), c_i32p, ctypes.POINTER(c_f32p)]
+    L.bertx_num_devices.restype = c_i32
+    L.bertx_num_devices.argtypes = [vp]
+    L.bertx_device_ordinal.restype = c_i32
+    L.bertx_device_ordinal.argtypes = [vp, c_i32]
+    L.bertx_hparams.argtypes = [vp, c_i32p]
+    L.bertx_forward_device.restype = c_i32
+    L.bertx_forward_device.argtypes = [vp, c_i32, vp, vp, c_i32, c_i32, c_i32, vp, vp]
+    L.bertx_reserve.restype = c_i32
+    L.bertx_reserve.argtypes = [vp, c_i32, c_i32, c_i32]
+    L.bertx_set_profiling.argtypes = [vp, c_i32]
+    L.bertx_reset_stats.argtypes = [vp]
+    L.bertx_kernel_stats.restype = c_i32
+    L.bertx_kernel_stats.argtypes = [vp, c_i32, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_int64),
+                                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), c_i32p]
+    L.bertx_quantize_file.restype = c_i32
+    L.bertx_quantize_file.argtypes = [ctypes.c_char_p, ctypes.c_char_p, c_i32]
+    L.bertx_test_gemm.restype = c_i32
+    L.bertx_test_gemm.argtypes = [c_i32, c_i32, c_i32, vp, c_f32p, c_i32, vp, c_i32, c_f32p, vp]
+    L.bertx_version.restype = ctypes.c_char_p
+    L.ggml_time_us.restype = ctypes.c_int64
+    if path is None:
+        _lib = L
+    return L
+
+
+def _as_i32p(a):
+    return a.ctypes.data_as(c_i32p)
+
+
+def _as_f32p(a):
+    return a.ctypes.data_as(c_f32p)
+
+
+class BertModel:
+    """Same surface as the reference client's BertModel (examples/sample_dylib.py:17-62)."""
+
+    N_THREADS = 6   # sample_dylib.py:7
+
+    def __init__(self, fname, lib=None):
+        self.lib = lib or load_lib()
+        self.ctx = self.lib.bert_load_from_file(fname.encode("utf-8"))
+        if not self.ctx:
+            raise RuntimeError("bert_load_from_file failed for " + fname)
+        self.n_embd = self.lib.bert_n_embd(self.ctx)
+        self.n_max_tokens = self.lib.bert_n_max_tokens(self.ctx)
+
+    def __del__(self):
+        if getattr(self, "ctx", None):
+            self.lib.bert_free(self.ctx)
+            self.ctx = None
+
+    def encode(self, sentences, batch_size=16):
+        input_is_string = isinstance(sentences, str)
+        if input_is_string:
+            sentences = [sentences]
+        n = len(sentences)
+        embeddings = np.zeros((n, self.n_embd), dtype=np.float32)
+        ptrs = (c_f32p * n)(*[e.ctypes.data_as(c_f32p) for e in embeddings])
+        texts = (ctypes.c_char_p * n)()
+        for j, s in enumerate(sentences):
+            texts[j] = s.encode("utf-8") if isinstance(s, str) else s
+        self.lib.bert_encode_batch(self.ctx, self.N_THREADS, batch_size, n, texts, ptrs)
+        return embeddings[0] if input_is_string else embeddings
+
+    # -- separate tokenization / forward (bert.h:56-85) --
+    def tokenize(self, text, n_max_tokens=None):
+        if isinstance(text, str):
+            text = text.encode("utf-8")
+        n_max = self.n_max_tokens if n_max_tokens is None else n_max_tokens
+        buf = np.zeros(max(n_max, 1), np.int32)
+        n = c_i32(0)
+        self.lib.bert_tokenize(self.ctx, text, _as_i32p(buf), ctypes.byref(n), n_max)
+        return [int(x) for x in buf[: min(n.value, n_max)]], n.value
+
+    def id_to_token(self, i):
+        return self.lib.bert_vocab_id_to_token(self.ctx, i)
+
+    def forward_batch(self, ids_list, fake=False, fill=0.0):
+        n = len(ids_list)
+        arrs = [np.ascontiguousarray(np.asarray(x, np.int32)) for x in ids_list]
+        lens = np.asarray([len(x) for x in arrs], np.int32)
+        out = np.full((n, self.n_embd), fill, np.float32)
+        tp = (c_i32p * n)(*[_as_i32p(a) for a in arrs])
+        op = (c_f32p * n)(*[o.ctypes.data_as(c_f32p) for o in out])
+        fn = self.lib.bert_forward_fake_batch if fake else self.lib.bert_forward_batch
+        fn(self.ctx, self.N_THREADS, n, tp, _as_i32p(lens), op)
+        return out
+
+    def forward(self, ids):
+        a = np.ascontiguousarray(np.asarray(ids, np.int32))
+        out = np.zeros(self.n_embd, np.float32)
+        self.lib.bert_forward(self.ctx, self.N_THREADS, _as_i32p(a), len(a), _as_f32p(out))
+        return out
+
+    def hparams(self):
+        hp = (c_i32 * 7)()
+        self.lib.bertx_hparams(self.ctx, hp)
+        return list(hp)
+
+    def kernel_stats(self):
+        out = []
+        i = 0
+        while True:
+            name = ctypes.c_char_p()
+            launches = ctypes.c_int64()
+            ms = ctypes.c_double()
+            work = ctypes.c_double()
+            flops = c_i32()
+            if self.lib.bertx_kernel_stats(self.ctx, i, ctypes.byref(name), ctypes.byref(launches),
+                                           ctypes.byref(ms), ctypes.byref(work), ctypes.byref(flops)) != 0:
+                break
+            out.append({"name": name.value.decode(), "launches": launches.value, "ms": ms.value,
+                        "work": work.value, "work_is_flops": bool(flops.value)})
+            i += 1
+        return out
+
+
+# ---------------------------------------------------------------------------
+# model files in the reference format
+# ---------------------------------------------------------------------------
+
+def tensor_names(n_layer):
+    """Tensor names and roles in converter order (convert-to-ggml.py iterates state_dict)."""
+    names = [("embeddings.word_embeddings.weight", "word"), ("embeddings.position_embeddings.weight", "pos"),
+             ("embeddings.token_type_embeddings.weight", "type"), ("embeddings.LayerNorm.weight", "ln_w"),
+             ("embeddings.LayerNorm.bias", "ln_b")]
+    for i in range(n_layer):
+        p = f"encoder.layer.{i}."
+        names += [(p + "attention.self.query.weight", "dd"), (p + "attention.self.query.bias", "d"),
+                  (p + "attention.self.key.weight", "dd"), (p + "attention.self.key.bias", "d"),
+                  (p + "attention.self.value.weight", "dd"), (p + "attention.self.value.bias", "d"),
+                  (p + "attention.output.dense.weight", "dd"), (p + "attention.output.dense.bias", "d"),
+                  (p + "attention.output.LayerNorm.weight", "ln_w"), (p + "attention.output.LayerNorm.bias", "ln_b"),
+                  (p + "intermediate.dense.weight", "fd"), (p + "intermediate.dense.bias", "f"),
+                  (p + "output.dense.weight", "df"), (p + "output.dense.bias", "d"),
+                  (p + "output.LayerNorm.weight", "ln_w"), (p + "output.LayerNorm.bias", "ln_b")]
+    return names
+
+
+def write_model(path, hp, vocab, tensors, ftype):
+    """hp: dict n_vocab,n_max_tokens,n_embd,n_intermediate,n_head,n_layer; tensors: name -> f32 array
+    (torch Linear layout [out][in]).  ftype 0 (f32) or 1 (f16): 2-D '*weight' tensors stored f16
+    like convert-to-ggml.py:96-101; everything else f32."""
+    assert ftype in (0, 1)
+    with open(path, "wb") as f:
+        f.write(struct.pack("<I", 0x67676D6C))
+        f.write(struct.pack("<7i", hp["n_vocab"], hp["n_max_tokens"], hp["n_embd"], hp["n_intermediate"],
+                            hp["n_head"], hp["n_layer"], ftype))
+        for w in vocab:
+            b = w.encode("utf-8")
+            f.write(struct.pack("<i", len(b)))
+            f.write(b)
+        for name, _ in tensor_names(hp["n_layer"]):
+            a = np.asarray(tensors[name], np.float32)
+            nd = a.ndim
+            if ftype == 1 and name.endswith(".weight") and nd == 2:
+                data, lt = a.astype(np.float16), 1
+            else:
+                data, lt = a, 0
+            nb = name.encode("utf-8")
+            f.write(struct.pack("<3i", nd, len(nb), lt))
+            for i in range(nd):
+                f.write(struct.pack("<i", a.shape[nd - 1 - i]))
+            f.write(nb)
+            f.write(np.ascontiguousarray(data).tobytes())
+
+
+ARCHS = {
+    # SURVEY.md §8 shapes (hparams as the HF configs of these checkpoints)
+    "all-MiniLM-L6-v2": dict(n_vocab=30522, n_max_tokens=512, n_embd=384, n_intermediate=1536, n_head=12, n_layer=6),
+    "bge-base-en-v1.5": dict(n_vocab=30522, n_max_tokens=512, n_embd=768, n_intermediate=3072, n_head=12, n_layer=12),
+    "bge-large-en-v1.5": dict(n_vocab=30522, n_max_tokens=512, n_embd=1024, n_intermediate=4096, n_head=16,
+                              n_layer=24),
+    "bge-base-zh-v1.5": dict(n_vocab=21128, n_max_tokens=512, n_embd=768, n_intermediate=3072, n_head=12,
+                             n_layer=12),
+}
+
+
+def synthetic_vocab(n_vocab):
+    """[PAD], [unused*], [UNK]=100, [CLS]=101, [SEP]=102, [MASK], then single-token words 'w<i>'
+    (so a text of k such words tokenizes to exactly k+2 ids)."""
+    v = ["[PAD]"] + ["[unused%d]" % i for i in range(99)] + ["[UNK]", "[CLS]", "[SEP]", "[MASK]"]
+    v += ["w%d" % i for i in range(n_vocab - len(v))]
+    return v[:n_vocab]
+
+
+def synthetic_tensors(hp, seed=1234):
+    """Random weights per SURVEY.md §8d: matrices and biases N(0, 0.02), LN gamma 1+N(0,0.02),
+    beta N(0, 0.02), numpy default_rng(seed)."""
+    rng = np.random.default_rng(seed)
+    d, f = hp["n_embd"], hp["n_intermediate"]
+    shapes = {"word": (hp["n_vocab"], d), "pos": (hp["n_max_tokens"], d), "type": (2, d), "dd": (d, d),
+              "fd": (f, d), "df": (d, f), "d": (d,), "f": (f,), "ln_w": (d,), "ln_b": (d,)}
+    out = {}
+    for name, role in tensor_names(hp["n_layer"]):
+        a = rng.standard_normal(shapes[role], dtype=np.float32) * np.float32(0.02)
+        if role == "ln_w":
+            a += np.float32(1.0)
+        out[name] = a
+    return out
+
+
+def synthetic_model(path, arch, ftype="q4_0", seed=1234, lib=None):
+    """Write a random-init model of `arch` in `ftype`.  Quantized files follow
+    run_conversions.sh:5-8: f32 -> f16 file -> quantize from the f16 values."""
+    hp = ARCHS[arch] if isinstance(arch, str) else arch
+    vocab = synthetic_vocab(hp["n_vocab"])
+    tensors = synthetic_tensors(hp, seed)
+    if ftype in ("f32", "f16"):
+        write_model(path, hp, vocab, tensors, FTYPE[ftype])
+        return path
+    tmp = path + ".f16.tmp"
+    write_model(tmp, hp, vocab, tensors, 1)
+    L = lib or load_lib()
+    rc = L.bertx_quantize_file(tmp.encode(), path.encode(), FTYPE[ftype])
+    os.remove(tmp)
+    if rc != 0:
+        raise RuntimeError("quantize failed")
+    return path
+
+
+def synthetic_ids(n, length, n_vocab, seed=7):
+    """Token ids per SURVEY.md §8d: uniform in [1000, V) with [CLS] first, [SEP] last."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for L in (length if hasattr(length, "__len__") else [length] * n):
+        x = rng.integers(1000, n_vocab, int(L), dtype=np.int32)
+        x[0], x[-1] = 101, 102
+        out.append(x)
+    return out

@@ -1,0 +1,390 @@
+// The drop-in C ABI (include/bert.h, reference bert.h:18-90) and the MI355X
+// extensions (include/bert_hip.h): context lifetime, tokenization, batching,
+// multi-GPU sharding of encode calls.  No CPU compute path: every forward runs
+// on the HIP kernels, and fails loudly when no device is present.
+#include "bert.h"
+#include "bert_hip.h"
+#include "ggml.h"
+
+#include "engine.h"
+#include "tokenizer.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <numeric>
+#include <string>
+#include <thread>
+#include <vector>
+
+using emb::Device;
+
+struct bert_ctx {
+    emb::HParams hp;
+    emb::Vocab vocab;
+    std::vector<std::unique_ptr<Device>> devices;
+    bool host_only = false;
+};
+
+namespace {
+
+constexpr int64_t kChunkTokens = 1 << 17;   // tokens per device forward (workspace bound)
+
+std::vector<int> parse_device_list(int n_visible)
+{
+    std::vector<int> out;
+    const char *env = std::getenv("BERT_DEVICES");
+    if (!env || !*env) {
+        for (int i = 0; i < n_visible; ++i) out.push_back(i);
+        return out;
+    }
+    std::string s(env);
+    size_t p = 0;
+    while (p <= s.size()) {
+        size_t q = s.find(',', p);
+        if (q == std::string::npos) q = s.size();
+        const std::string tok = s.substr(p, q - p);
+        if (!tok.empty()) {
+            const int v = std::atoi(tok.c_str());
+            if (v >= 0 && v < n_visible && std::find(out.begin(), out.end(), v) == out.end()) out.push_back(v);
+        }
+        p = q + 1;
+    }
+    return out;
+}
+
+// FLOP-proportional cost of one sentence of length L (GEMMs + attention).
+double sentence_cost(const emb::HParams &hp, int L)
+{
+    const double d = hp.n_embd, f = hp.n_intermediate;
+    return (double)L * (8.0 * d * d + 4.0 * d * f) + 4.0 * (double)L * L * d;
+}
+
+// Runs n sentences on the context's GPUs.  Work is split by cost over devices
+// (longest-processing-time first); each device walks its sentences in length
+// order in chunks of <= kChunkTokens.  Results are independent of the split:
+// every kernel computes a sentence from its own tokens only.
+int run_forward(bert_ctx *ctx, const int32_t *const *toks, const int32_t *lens, float *const *outs, int n)
+{
+    if (ctx->devices.empty()) {
+        std::fprintf(stderr, "libbert: no HIP device in this context (BERT_HOST_ONLY); forward unavailable\n");
+        return -1;
+    }
+    if (n <= 0) return 0;
+    const int nd = (int)ctx->devices.size();
+    std::vector<int> order((size_t)n);
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return lens[a] > lens[b]; });
+    std::vector<std::vector<int>> assign((size_t)nd);
+    std::vector<double> load((size_t)nd, 0.0);
+    for (int idx : order) {
+        const int dv = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+        assign[(size_t)dv].push_back(idx);
+        load[(size_t)dv] += sentence_cost(ctx->hp, lens[idx]);
+    }
+    std::vector<int> rcs((size_t)nd, 0);
+    auto work = [&](int dv) {
+        Device &D = *ctx->devices[(size_t)dv];
+        std::lock_guard<std::mutex> lk(D.mutex());
+        const std::vector<int> &mine = assign[(size_t)dv];
+        std::vector<const int32_t *> tp;
+        std::vector<int32_t> lp;
+        std::vector<float *> op;
+        size_t i = 0;
+        while (i < mine.size()) {
+            tp.clear(); lp.clear(); op.clear();
+            int64_t tok = 0;
+            while (i < mine.size() && (tp.empty() || tok + lens[mine[i]] <= kChunkTokens)) {
+                const int idx = mine[i++];
+                tp.push_back(toks[idx]); lp.push_back(lens[idx]); op.push_back(outs[idx]);
+                tok += lens[idx];
+            }
+            const int rc = D.forward_host(tp.data(), lp.data(), (int)tp.size(), op.data());
+            if (rc != 0) { rcs[(size_t)dv] = rc; return; }
+        }
+    };
+    int used = 0;
+    for (int dv = 0; dv < nd; ++dv) used += assign[(size_t)dv].empty() ? 0 : 1;
+    if (used <= 1) {
+        for (int dv = 0; dv < nd; ++dv) if (!assign[(size_t)dv].empty()) work(dv);
+    } else {
+        std::vector<std::thread> th;
+        for (int dv = 0; dv < nd; ++dv) if (!assign[(size_t)dv].empty()) th.emplace_back(work, dv);
+        for (auto &t : th) t.join();
+    }
+    for (int rc : rcs) if (rc != 0) {
+        std::fprintf(stderr, "libbert: forward failed (%d)\n", rc);
+        return rc;
+    }
+    return 0;
+}
+
+void print_usage(char **argv, const bert_params &p)
+{
+    std::fprintf(stderr, "usage: %s [options]\n\noptions:\n", argv[0]);
+    std::fprintf(stderr, "  -h, --help            show this help message and exit\n");
+    std::fprintf(stderr, "  -t N, --threads N     host threads (tokenizer pool) (default: %d)\n", p.n_threads);
+    std::fprintf(stderr, "  -p PROMPT, --prompt PROMPT\n                        prompt text (default: %s)\n", p.prompt);
+    std::fprintf(stderr, "  --port p              port to bind in server mode (default: %d)\n", p.port);
+    std::fprintf(stderr, "  -m FNAME, --model FNAME\n                        model path (default: %s)\n", p.model);
+    std::fprintf(stderr, "  environment: BERT_DEVICES=0,1,... (GPUs to use), BERT_HOST_ONLY=1\n\n");
+}
+
+}  // namespace
+
+extern "C" {
+
+// ---------------------------------------------------------------------------
+// ggml time shims (examples/main.cpp, test_batch_encode.cpp call these)
+// ---------------------------------------------------------------------------
+static std::chrono::steady_clock::time_point g_t0 = std::chrono::steady_clock::now();
+void ggml_time_init(void) { g_t0 = std::chrono::steady_clock::now(); }
+int64_t ggml_time_us(void)
+{
+    return std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - g_t0).count();
+}
+int64_t ggml_time_ms(void) { return ggml_time_us() / 1000; }
+
+// ---------------------------------------------------------------------------
+// bert.h
+// ---------------------------------------------------------------------------
+
+bool bert_params_parse(int argc, char **argv, bert_params &params)
+{
+    for (int i = 1; i < argc; ++i) {
+        const std::string a = argv[i];
+        const bool has_val = i + 1 < argc;
+        if ((a == "-t" || a == "--threads") && has_val) params.n_threads = std::stoi(argv[++i]);
+        else if ((a == "-p" || a == "--prompt") && has_val) params.prompt = argv[++i];
+        else if (a == "--port" && has_val) params.port = std::stoi(argv[++i]);
+        else if ((a == "-m" || a == "--model") && has_val) params.model = argv[++i];
+        else if (a == "-h" || a == "--help") { print_usage(argv, params); std::exit(0); }
+        else {
+            std::fprintf(stderr, "error: unknown argument: %s\n", a.c_str());
+            print_usage(argv, params);
+            std::exit(0);
+        }
+    }
+    return true;
+}
+
+struct bert_ctx *bert_load_from_file(const char *fname)
+{
+    std::printf("bert_load_from_file: loading model from '%s' - please wait ...\n", fname);
+    emb::HostModel m;
+    std::string err;
+    if (!emb::load_model_file(fname, m, err, true)) {
+        std::fprintf(stderr, "bert_load_from_file: %s\n", err.c_str());
+        return nullptr;
+    }
+    std::unique_ptr<bert_ctx> ctx(new bert_ctx);
+    ctx->hp = m.hp;
+    ctx->vocab.build(m.vocab);
+    const char *ho = std::getenv("BERT_HOST_ONLY");
+    const bool host_only = ho && *ho && std::strcmp(ho, "0") != 0;
+    const std::vector<int> devs = host_only ? std::vector<int>() : parse_device_list(emb::hip_device_count());
+    if (devs.empty()) {
+        if (!host_only) {
+            std::fprintf(stderr, "bert_load_from_file: no HIP (gfx950) device available -- libbert.so has no CPU "
+                                 "compute path (set BERT_HOST_ONLY=1 for a tokenizer-only context)\n");
+            return nullptr;
+        }
+        ctx->host_only = true;
+        std::printf("bert_load_from_file: host-only context (tokenizer only, no forward)\n");
+        return ctx.release();
+    }
+    std::vector<std::unique_ptr<Device>> made(devs.size());
+    {
+        std::vector<std::thread> th;
+        for (size_t i = 0; i < devs.size(); ++i)
+            th.emplace_back([&, i] { made[i].reset(new Device(devs[i], m)); });
+        for (auto &t : th) t.join();
+    }
+    for (auto &d : made) {
+        if (!d->ok()) {
+            std::fprintf(stderr, "bert_load_from_file: device %d initialisation failed\n", d->ordinal());
+            return nullptr;
+        }
+        ctx->devices.push_back(std::move(d));
+    }
+    std::printf("bert_load_from_file: MI355X engine on %zu HIP device(s)\n", ctx->devices.size());
+    return ctx.release();
+}
+
+void bert_free(bert_ctx *ctx) { delete ctx; }
+
+int32_t bert_n_embd(bert_ctx *ctx) { return ctx->hp.n_embd; }
+int32_t bert_n_max_tokens(bert_ctx *ctx) { return ctx->hp.n_max_tokens; }
+const char *bert_vocab_id_to_token(bert_ctx *ctx, bert_vocab_id id) { return ctx->vocab.id_to_token(id); }
+
+void bert_tokenize(struct bert_ctx *ctx, const char *text, bert_vocab_id *tokens, int32_t *n_tokens,
+                   int32_t n_max_tokens)
+{
+    *n_tokens = ctx->vocab.tokenize(text, n_max_tokens, tokens, n_max_tokens > 0 ? n_max_tokens : 0);
+}
+
+void bert_forward_batch(bert_ctx *ctx, int32_t n_threads, int32_t n_batch_size, bert_vocab_id **batch_tokens,
+                        int32_t *n_tokens, float **batch_embeddings)
+{
+    (void)n_threads;
+    if (!batch_embeddings || n_batch_size <= 0) return;   // reference memory-measurement mode: no output
+    int32_t mx = 0;
+    for (int i = 0; i < n_batch_size; ++i) mx = std::max(mx, n_tokens[i]);
+    if (mx > ctx->hp.n_max_tokens) {
+        std::fprintf(stderr, "Too many tokens, maximum is %d\n", ctx->hp.n_max_tokens);
+        return;
+    }
+    run_forward(ctx, batch_tokens, n_tokens, batch_embeddings, n_batch_size);
+}
+
+void bert_forward(struct bert_ctx *ctx, int32_t n_threads, bert_vocab_id *tokens, int32_t n_tokens, float *embeddings)
+{
+    bert_forward_batch(ctx, n_threads, 1, &tokens, &n_tokens, embeddings ? &embeddings : nullptr);
+}
+
+void bert_forward_fake_batch(bert_ctx *ctx, int32_t n_threads, int32_t n_batch_size, bert_vocab_id **batch_tokens,
+                             int32_t *n_tokens, float **batch_embeddings)
+{
+    (void)n_threads;
+    std::printf("using function bert_forward_fake_batch\n");
+    if (!batch_embeddings || n_batch_size <= 0) return;
+    // the reference stops at the first over-long input, after writing the ones before it
+    int n_ok = 0;
+    while (n_ok < n_batch_size && n_tokens[n_ok] <= ctx->hp.n_max_tokens) ++n_ok;
+    run_forward(ctx, batch_tokens, n_tokens, batch_embeddings, n_ok);
+    if (n_ok < n_batch_size) std::fprintf(stderr, "Too many tokens, maximum is %d\n", ctx->hp.n_max_tokens);
+}
+
+void bert_encode_batch(struct bert_ctx *ctx, int32_t n_threads, int32_t n_batch_size, int32_t n_inputs,
+                       const char **texts, float **embeddings)
+{
+    if (n_inputs <= 0) return;
+    const int32_t N = ctx->hp.n_max_tokens;
+    std::vector<int32_t> ids((size_t)n_inputs * N);
+    std::vector<int32_t> lens((size_t)n_inputs);
+    const int nt = std::max(1, std::min<int>(n_threads > 0 ? n_threads : 1, n_inputs / 8 + 1));
+    auto tok = [&](int t0) {
+        for (int i = t0; i < n_inputs; i += nt)
+            lens[(size_t)i] = ctx->vocab.tokenize(texts[i], N, ids.data() + (size_t)i * N, N);
+    };
+    if (nt == 1) tok(0);
+    else {
+        std::vector<std::thread> th;
+        for (int t = 0; t < nt; ++t) th.emplace_back(tok, t);
+        for (auto &t : th) t.join();
+    }
+    // which inputs the reference's chunking refuses (bert.cpp:1408-1443)
+    std::vector<char> ok((size_t)n_inputs, 1);
+    if (n_batch_size == n_inputs || n_batch_size <= 0) {
+        if (*std::max_element(lens.begin(), lens.end()) > N) {
+            std::fprintf(stderr, "Too many tokens, maximum is %d\n", N);
+            return;
+        }
+    } else {
+        std::vector<int> idx((size_t)n_inputs);
+        std::iota(idx.begin(), idx.end(), 0);
+        std::sort(idx.begin(), idx.end(), [&](int a, int b) { return lens[(size_t)a] < lens[(size_t)b]; });
+        for (int s = 0; s < n_inputs; s += n_batch_size) {
+            const int e = std::min(n_inputs, s + n_batch_size);
+            if (lens[(size_t)idx[(size_t)e - 1]] > N) {
+                std::fprintf(stderr, "Too many tokens, maximum is %d\n", N);
+                for (int j = s; j < e; ++j) ok[(size_t)idx[(size_t)j]] = 0;
+            }
+        }
+    }
+    std::vector<const int32_t *> tp;
+    std::vector<int32_t> lp;
+    std::vector<float *> op;
+    for (int i = 0; i < n_inputs; ++i) {
+        if (!ok[(size_t)i]) continue;
+        tp.push_back(ids.data() + (size_t)i * N);
+        lp.push_back(lens[(size_t)i]);
+        op.push_back(embeddings[i]);
+    }
+    run_forward(ctx, tp.data(), lp.data(), op.data(), (int)tp.size());
+}
+
+void bert_encode(struct bert_ctx *ctx, int32_t n_threads, const char *texts, float *embeddings)
+{
+    bert_encode_batch(ctx, n_threads, 1, 1, &texts, &embeddings);
+}
+
+// ---------------------------------------------------------------------------
+// bert_hip.h
+// ---------------------------------------------------------------------------
+
+int32_t bertx_num_devices(struct bert_ctx *ctx) { return (int32_t)ctx->devices.size(); }
+
+int32_t bertx_device_ordinal(struct bert_ctx *ctx, int32_t slot)
+{
+    return (slot >= 0 && slot < (int32_t)ctx->devices.size()) ? ctx->devices[(size_t)slot]->ordinal() : -1;
+}
+
+void bertx_hparams(struct bert_ctx *ctx, int32_t *o)
+{
+    o[0] = ctx->hp.n_vocab; o[1] = ctx->hp.n_max_tokens; o[2] = ctx->hp.n_embd; o[3] = ctx->hp.n_intermediate;
+    o[4] = ctx->hp.n_head; o[5] = ctx->hp.n_layer; o[6] = ctx->hp.ftype;
+}
+
+int32_t bertx_reserve(struct bert_ctx *ctx, int32_t slot, int32_t total_tokens, int32_t n_seqs)
+{
+    if (slot < 0 || slot >= (int32_t)ctx->devices.size()) return -1;
+    Device &D = *ctx->devices[(size_t)slot];
+    std::lock_guard<std::mutex> lk(D.mutex());
+    (void)hipSetDevice(D.ordinal());
+    return D.reserve(total_tokens, n_seqs) ? 0 : -1;
+}
+
+int32_t bertx_forward_device(struct bert_ctx *ctx, int32_t slot, const int32_t *d_ids, const int32_t *d_cu,
+                             int32_t n_seqs, int32_t max_len, int32_t total_tokens, float *d_out, void *stream)
+{
+    if (slot < 0 || slot >= (int32_t)ctx->devices.size()) return -1;
+    if (max_len > ctx->hp.n_max_tokens || max_len <= 0) return -4;
+    Device &D = *ctx->devices[(size_t)slot];
+    std::lock_guard<std::mutex> lk(D.mutex());
+    (void)hipSetDevice(D.ordinal());
+    return D.forward(d_ids, d_cu, n_seqs, max_len, total_tokens, d_out, stream ? (hipStream_t)stream : D.stream());
+}
+
+void bertx_set_profiling(struct bert_ctx *ctx, int32_t on)
+{
+    for (auto &d : ctx->devices) d->set_profiling(on != 0);
+}
+
+void bertx_reset_stats(struct bert_ctx *ctx)
+{
+    for (auto &d : ctx->devices) d->reset_stats();
+}
+
+int32_t bertx_kernel_stats(struct bert_ctx *ctx, int32_t idx, const char **name, int64_t *launches, double *total_ms,
+                           double *work, int32_t *work_is_flops)
+{
+    if (idx < 0 || idx >= emb::K_NUM_CLASSES) return -1;
+    int64_t l = 0;
+    double ms = 0, w = 0;
+    for (auto &d : ctx->devices) {
+        d->collect_stats();
+        l += d->stats(idx).launches;
+        ms += d->stats(idx).ms;
+        w += d->stats(idx).work;
+    }
+    if (name) *name = emb::kclass_name(idx);
+    if (launches) *launches = l;
+    if (total_ms) *total_ms = ms;
+    if (work) *work = w;
+    if (work_is_flops)
+        *work_is_flops = (idx == emb::K_EMBED_LN || idx == emb::K_LAYERNORM || idx == emb::K_POOL_L2) ? 0 : 1;
+    return 0;
+}
+
+int32_t bertx_quantize_file(const char *fin, const char *fout, int32_t itype)
+{
+    return emb::quantize_file(fin, fout, itype, false);
+}
+
+const char *bertx_version(void) { return "embeddings.cpp_amd 0.1 (gfx950)"; }
+
+}  // extern "C"

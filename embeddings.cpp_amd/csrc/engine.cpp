@@ -1,0 +1,486 @@
+// Per-GPU engine: weight repack + upload, workspace, forward launch sequence,
+// live per-kernel timing.  See kernels.h for the HBM layouts.
+#include "engine.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+
+namespace emb {
+
+#define HIP_OK(expr)                                                                                     \
+    do {                                                                                                 \
+        hipError_t e_ = (expr);                                                                          \
+        if (e_ != hipSuccess) {                                                                          \
+            std::fprintf(stderr, "libbert: HIP error %s at %s:%d (%s)\n", hipGetErrorString(e_), __FILE__, \
+                         __LINE__, #expr);                                                               \
+            return false;                                                                                \
+        }                                                                                                \
+    } while (0)
+
+#define HIP_RC(expr)                                                                                     \
+    do {                                                                                                 \
+        hipError_t e_ = (expr);                                                                          \
+        if (e_ != hipSuccess) {                                                                          \
+            std::fprintf(stderr, "libbert: HIP error %s at %s:%d (%s)\n", hipGetErrorString(e_), __FILE__, \
+                         __LINE__, #expr);                                                               \
+            return -1;                                                                                   \
+        }                                                                                                \
+    } while (0)
+
+const char *kclass_name(int k)
+{
+    static const char *names[K_NUM_CLASSES] = {"embed_ln", "gemm_qkv", "attention", "gemm_attn_out",
+                                               "layernorm", "gemm_ffn_up", "gemm_ffn_down", "pool_l2"};
+    return (k >= 0 && k < K_NUM_CLASSES) ? names[k] : "?";
+}
+
+int hip_device_count()
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return n;
+}
+
+namespace {
+
+inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+// One host-side staged buffer of the replica.
+struct Piece {
+    std::vector<uint8_t> bytes;
+    size_t off = 0;
+};
+
+// Linear weight [N][K] (file rows) -> K-step-major device layout (kernels.h).
+void repack_linear(const std::vector<const HostTensor *> &parts, int fmt_dev, Piece &qs, Piece &dpl, Piece &mpl,
+                   int &N_out, int &K_out)
+{
+    const int K = parts[0]->ne0;
+    int N = 0;
+    for (const HostTensor *t : parts) N += t->ne1;
+    N_out = N;
+    K_out = K;
+    const int KS = K / 64;
+    if (fmt_dev == FMT_F16) {
+        qs.bytes.assign((size_t)N * K * 2, 0);
+        uint16_t *dst = (uint16_t *)qs.bytes.data();
+        std::vector<float> row((size_t)K);
+        int n = 0;
+        for (const HostTensor *t : parts) {
+            const size_t rb = fmt_row_bytes(t->fmt, K);
+            for (int r = 0; r < t->ne1; ++r, ++n) {
+                const uint8_t *src = t->bytes.data() + rb * r;
+                for (int k = 0; k < K; ++k) {
+                    uint16_t h;
+                    if (t->fmt == FMT_F16) std::memcpy(&h, src + 2 * k, 2);
+                    else { float f; std::memcpy(&f, src + 4 * k, 4); h = f32_to_f16(f); }
+                    dst[((size_t)(k / 64) * N + n) * 64 + (k % 64)] = h;
+                }
+            }
+        }
+        return;
+    }
+    const size_t nblk = (size_t)N * (K / 32);
+    dpl.bytes.assign(nblk * 2, 0);
+    if (fmt_dev == FMT_Q4_1) mpl.bytes.assign(nblk * 2, 0);
+    qs.bytes.assign(nblk * (fmt_dev == FMT_Q8_0 ? 32 : 16), 0);
+    uint16_t *dd = (uint16_t *)dpl.bytes.data();
+    uint16_t *mm = fmt_dev == FMT_Q4_1 ? (uint16_t *)mpl.bytes.data() : nullptr;
+    int n = 0;
+    for (const HostTensor *t : parts) {
+        const size_t rb = fmt_row_bytes(t->fmt, K), bb = fmt_block_bytes(t->fmt);
+        for (int r = 0; r < t->ne1; ++r, ++n) {
+            for (int b = 0; b < K / 32; ++b) {
+                const uint8_t *blk = t->bytes.data() + rb * r + bb * b;
+                const size_t di = ((size_t)(b / 2) * N + n) * 2 + (b & 1);
+                (void)KS;
+                std::memcpy(&dd[di], blk, 2);
+                if (fmt_dev == FMT_Q8_0) {
+                    const int8_t *q = (const int8_t *)(blk + 2);
+                    uint8_t *o = qs.bytes.data() + di * 32;
+                    for (int g = 0; g < 8; ++g) {
+                        const int order[4] = {0, 2, 1, 3};
+                        for (int i = 0; i < 4; ++i) o[4 * g + i] = (uint8_t)((uint8_t)q[4 * g + order[i]] ^ 0x80u);
+                    }
+                } else {
+                    const uint8_t *nib = blk + (fmt_dev == FMT_Q4_1 ? 4 : 2);
+                    if (mm) std::memcpy(&mm[di], blk + 2, 2);
+                    uint32_t *o = (uint32_t *)(qs.bytes.data() + di * 16);
+                    for (int w = 0; w < 4; ++w) {
+                        uint32_t word = 0;
+                        for (int i = 0; i < 8; ++i) {
+                            const int e = 8 * w + i;
+                            const uint32_t q = e < 16 ? (nib[e] & 15u) : (uint32_t)(nib[e - 16] >> 4);
+                            word |= q << (4 * (i / 2) + 16 * (i % 2));
+                        }
+                        o[w] = word;
+                    }
+                }
+            }
+        }
+    }
+}
+
+// Embedding table in its file format -> aligned planes.
+void repack_table(const HostTensor &t, Piece &qs, Piece &dpl, Piece &mpl)
+{
+    const int rows = t.ne1, cols = t.ne0;
+    if (t.fmt == FMT_F32 || t.fmt == FMT_F16) {
+        qs.bytes = t.bytes;
+        return;
+    }
+    const size_t nblk = (size_t)rows * (cols / 32), bb = fmt_block_bytes(t.fmt);
+    const size_t qb = t.fmt == FMT_Q8_0 ? 32 : 16;
+    qs.bytes.assign(nblk * qb, 0);
+    dpl.bytes.assign(nblk * 2, 0);
+    if (t.fmt == FMT_Q4_1) mpl.bytes.assign(nblk * 2, 0);
+    for (size_t i = 0; i < nblk; ++i) {
+        const uint8_t *blk = t.bytes.data() + i * bb;
+        std::memcpy(dpl.bytes.data() + 2 * i, blk, 2);
+        if (t.fmt == FMT_Q4_1) {
+            std::memcpy(mpl.bytes.data() + 2 * i, blk + 2, 2);
+            std::memcpy(qs.bytes.data() + 16 * i, blk + 4, 16);
+        } else {
+            std::memcpy(qs.bytes.data() + qb * i, blk + 2, qb);
+        }
+    }
+}
+
+}  // namespace
+
+Device::Device(int ordinal, const HostModel &m) : ordinal_(ordinal), hp_(m.hp)
+{
+    if (hipSetDevice(ordinal) != hipSuccess || hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) {
+        std::fprintf(stderr, "libbert: cannot initialise HIP device %d\n", ordinal);
+        return;
+    }
+    upload(m);
+}
+
+Device::~Device()
+{
+    (void)hipSetDevice(ordinal_);
+    if (stream_) (void)hipStreamSynchronize(stream_);
+    for (auto &p : pending_) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
+    for (auto e : free_events_) (void)hipEventDestroy(e);
+    if (arena_) (void)hipFree(arena_);
+    if (ws_) (void)hipFree(ws_);
+    if (h_ids_) (void)hipHostFree(h_ids_);
+    if (h_cu_) (void)hipHostFree(h_cu_);
+    if (h_out_) (void)hipHostFree(h_out_);
+    if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+void Device::upload(const HostModel &m)
+{
+    const int d = hp_.n_embd, f = hp_.n_intermediate;
+    if (d % 64 || d > 1024 || f % 64 || (d / hp_.n_head != 32 && d / hp_.n_head != 64)) {
+        std::fprintf(stderr, "libbert: unsupported shape n_embd=%d n_intermediate=%d head_dim=%d "
+                             "(need n_embd %% 64 == 0, n_embd <= 1024, head_dim 32 or 64)\n",
+                     d, f, d / hp_.n_head);
+        return;
+    }
+    wfmt_ = (hp_.ftype == FMT_F32 || hp_.ftype == FMT_F16) ? FMT_F16 : hp_.ftype;
+    std::vector<Piece> pieces;
+    pieces.reserve(16 + 24 * (size_t)hp_.n_layer);
+    auto add = [&](Piece &&p) -> size_t { pieces.push_back(std::move(p)); return pieces.size() - 1; };
+    auto vec = [&](const HostTensor &t) -> size_t { Piece p; p.bytes = t.bytes; return add(std::move(p)); };
+    auto vec_cat = [&](std::initializer_list<const HostTensor *> ts) -> size_t {
+        Piece p;
+        for (const HostTensor *t : ts) p.bytes.insert(p.bytes.end(), t->bytes.begin(), t->bytes.end());
+        return add(std::move(p));
+    };
+    struct TabIdx { size_t q, d, m; };
+    auto table = [&](const HostTensor &t) -> TabIdx {
+        Piece q, dd, mm;
+        repack_table(t, q, dd, mm);
+        TabIdx r;
+        r.q = add(std::move(q)); r.d = add(std::move(dd)); r.m = add(std::move(mm));
+        return r;
+    };
+    struct LinIdx { size_t q, d, m; int N, K; };
+    auto linear = [&](std::vector<const HostTensor *> parts) -> LinIdx {
+        Piece q, dd, mm;
+        LinIdx r;
+        repack_linear(parts, wfmt_, q, dd, mm, r.N, r.K);
+        r.q = add(std::move(q)); r.d = add(std::move(dd)); r.m = add(std::move(mm));
+        return r;
+    };
+    const TabIdx tw = table(m.word), tt = table(m.ttype), tp = table(m.pos);
+    const size_t lnw = vec(m.ln_e_w), lnb = vec(m.ln_e_b);
+    struct LIdx { LinIdx qkv, o, up, down; size_t bqkv, bo, bup, bdown, l1w, l1b, l2w, l2b; };
+    std::vector<LIdx> li((size_t)hp_.n_layer);
+    for (int l = 0; l < hp_.n_layer; ++l) {
+        const HostLayer &L = m.layers[(size_t)l];
+        LIdx &x = li[(size_t)l];
+        x.qkv = linear({&L.q_w, &L.k_w, &L.v_w});
+        x.o = linear({&L.o_w});
+        x.up = linear({&L.i_w});
+        x.down = linear({&L.o2_w});
+        x.bqkv = vec_cat({&L.q_b, &L.k_b, &L.v_b});
+        x.bo = vec(L.o_b); x.bup = vec(L.i_b); x.bdown = vec(L.o2_b);
+        x.l1w = vec(L.ln_att_w); x.l1b = vec(L.ln_att_b); x.l2w = vec(L.ln_out_w); x.l2b = vec(L.ln_out_b);
+    }
+    size_t total = 0;
+    for (Piece &p : pieces) { p.off = total; total += align_up(p.bytes.size(), 256); }
+    if (hipMalloc((void **)&arena_, total ? total : 256) != hipSuccess) {
+        std::fprintf(stderr, "libbert: hipMalloc of %zu bytes of weights failed on device %d\n", total, ordinal_);
+        arena_ = nullptr;
+        return;
+    }
+    arena_size_ = total;
+    for (Piece &p : pieces)
+        if (!p.bytes.empty() && hipMemcpy(arena_ + p.off, p.bytes.data(), p.bytes.size(), hipMemcpyHostToDevice) != hipSuccess) {
+            std::fprintf(stderr, "libbert: weight upload failed on device %d\n", ordinal_);
+            return;
+        }
+    auto P = [&](size_t i) -> void * { return pieces[i].bytes.empty() ? nullptr : (void *)(arena_ + pieces[i].off); };
+    auto mk_table = [&](const TabIdx &x, const HostTensor &t) {
+        DevTable r;
+        r.fmt = t.fmt; r.rows = t.ne1; r.cols = t.ne0;
+        r.qs = P(x.q); r.d = (const uint16_t *)P(x.d); r.m = (const uint16_t *)P(x.m);
+        return r;
+    };
+    word_ = mk_table(tw, m.word);
+    type_ = mk_table(tt, m.ttype);
+    pos_ = mk_table(tp, m.pos);
+    ln_e_w_ = (float *)P(lnw);
+    ln_e_b_ = (float *)P(lnb);
+    auto mk_lin = [&](const LinIdx &x) {
+        DevWeight w;
+        w.fmt = wfmt_; w.N = x.N; w.K = x.K;
+        w.qs = P(x.q); w.d = (const uint16_t *)P(x.d); w.m = (const uint16_t *)P(x.m);
+        return w;
+    };
+    layers_.resize((size_t)hp_.n_layer);
+    for (int l = 0; l < hp_.n_layer; ++l) {
+        const LIdx &x = li[(size_t)l];
+        DevLayer &D = layers_[(size_t)l];
+        D.qkv = mk_lin(x.qkv); D.o = mk_lin(x.o); D.up = mk_lin(x.up); D.down = mk_lin(x.down);
+        D.b_qkv = (float *)P(x.bqkv); D.b_o = (float *)P(x.bo); D.b_up = (float *)P(x.bup); D.b_down = (float *)P(x.bdown);
+        D.ln1_w = (float *)P(x.l1w); D.ln1_b = (float *)P(x.l1b); D.ln2_w = (float *)P(x.l2w); D.ln2_b = (float *)P(x.l2b);
+    }
+    ok_ = true;
+}
+
+bool Device::reserve(int64_t tokens, int64_t seqs)
+{
+    if (tokens <= cap_tokens_ && seqs <= cap_seqs_) return true;
+    HIP_OK(hipSetDevice(ordinal_));
+    HIP_OK(hipStreamSynchronize(stream_));
+    const int64_t nt = std::max<int64_t>(align_up((size_t)std::max(tokens, cap_tokens_), 4096), 4096);
+    const int64_t ns = std::max<int64_t>(align_up((size_t)std::max(seqs, cap_seqs_), 256), 256);
+    const int64_t rows = nt + GEMM_BM + 256;   // padding rows for tile overrun (kernels read, never trust)
+    const int64_t d = hp_.n_embd, f = hp_.n_intermediate;
+    size_t off = 0;
+    auto take = [&](size_t bytes) { size_t o = off; off += align_up(bytes, 256); return o; };
+    const size_t o_x32 = take(rows * d * 4), o_y32 = take(rows * d * 4), o_xh = take(rows * d * 2);
+    const size_t o_qkv = take(rows * 3 * d * 2), o_att = take(rows * d * 2), o_ffn = take(rows * f * 2);
+    const size_t o_ids = take(rows * 4), o_cu = take((ns + 1) * 4), o_out = take(ns * d * 4);
+    if (ws_) { (void)hipFree(ws_); ws_ = nullptr; }
+    if (h_ids_) { (void)hipHostFree(h_ids_); h_ids_ = nullptr; }
+    if (h_cu_) { (void)hipHostFree(h_cu_); h_cu_ = nullptr; }
+    if (h_out_) { (void)hipHostFree(h_out_); h_out_ = nullptr; }
+    cap_tokens_ = cap_seqs_ = 0;
+    HIP_OK(hipMalloc((void **)&ws_, off));
+    HIP_OK(hipMemset(ws_, 0, off));
+    x32_ = (float *)(ws_ + o_x32); y32_ = (float *)(ws_ + o_y32); xh_ = (uint16_t *)(ws_ + o_xh);
+    qkv_ = (uint16_t *)(ws_ + o_qkv); att_ = (uint16_t *)(ws_ + o_att); ffn_ = (uint16_t *)(ws_ + o_ffn);
+    d_ids_ = (int32_t *)(ws_ + o_ids); d_cu_ = (int32_t *)(ws_ + o_cu); d_out_ = (float *)(ws_ + o_out);
+    HIP_OK(hipHostMalloc((void **)&h_ids_, nt * 4, hipHostMallocDefault));
+    HIP_OK(hipHostMalloc((void **)&h_cu_, (ns + 1) * 4, hipHostMallocDefault));
+    HIP_OK(hipHostMalloc((void **)&h_out_, ns * d * 4, hipHostMallocDefault));
+    cap_tokens_ = nt;
+    cap_seqs_ = ns;
+    return true;
+}
+
+hipEvent_t Device::get_event()
+{
+    if (!free_events_.empty()) { hipEvent_t e = free_events_.back(); free_events_.pop_back(); return e; }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+}
+
+void Device::begin(int cls, hipStream_t s, hipEvent_t &a)
+{
+    (void)cls;
+    a = nullptr;
+    if (!profiling_) return;
+    a = get_event();
+    (void)hipEventRecord(a, s);
+}
+
+void Device::end(int cls, hipStream_t s, hipEvent_t a, double work)
+{
+    if (!profiling_ || !a) return;
+    hipEvent_t b = get_event();
+    (void)hipEventRecord(b, s);
+    pending_.push_back({cls, a, b, work});
+}
+
+void Device::collect_stats()
+{
+    (void)hipSetDevice(ordinal_);
+    for (auto &p : pending_) {
+        (void)hipEventSynchronize(p.b);
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+            stats_[p.cls].launches += 1;
+            stats_[p.cls].ms += ms;
+            stats_[p.cls].work += p.work;
+        }
+        free_events_.push_back(p.a);
+        free_events_.push_back(p.b);
+    }
+    pending_.clear();
+}
+
+void Device::reset_stats()
+{
+    collect_stats();
+    for (auto &s : stats_) s = KStats();
+}
+
+int Device::forward(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, int max_len, int T, float *d_out,
+                    hipStream_t s)
+{
+    if (!ok_) return -3;
+    if (T > cap_tokens_ || n_seqs > cap_seqs_) return -2;
+    if (T <= 0 || n_seqs <= 0) return 0;
+    const int d = hp_.n_embd, f = hp_.n_intermediate;
+    const int M = (int)align_up((size_t)T, GEMM_BM);
+    const double t = (double)T;
+    hipEvent_t ev;
+
+    begin(K_EMBED_LN, s, ev);
+    launch_embed_ln(word_, type_, pos_, ln_e_w_, ln_e_b_, d_ids, d_cu, n_seqs, max_len, d, x32_, xh_, s);
+    end(K_EMBED_LN, s, ev, t * (4.0 + 3.0 * d * 2.0 + 6.0 * d));
+
+    const double att_flop = 4.0 * (double)d * t * (double)max_len;   // exact when all lengths are equal
+    for (int l = 0; l < hp_.n_layer; ++l) {
+        const DevLayer &L = layers_[(size_t)l];
+        begin(K_GEMM_QKV, s, ev);
+        launch_gemm(L.qkv, xh_, M, L.b_qkv, EPI_BIAS_F16, nullptr, qkv_, s);
+        end(K_GEMM_QKV, s, ev, 2.0 * t * 3.0 * d * d);
+
+        begin(K_ATTENTION, s, ev);
+        launch_attention(qkv_, d_cu, n_seqs, max_len, hp_.n_head, d, att_, s);
+        end(K_ATTENTION, s, ev, att_flop);
+
+        begin(K_GEMM_O, s, ev);
+        launch_gemm(L.o, att_, M, L.b_o, EPI_BIAS_RES_F32, x32_, y32_, s);
+        end(K_GEMM_O, s, ev, 2.0 * t * d * d);
+
+        begin(K_LAYERNORM, s, ev);
+        launch_layernorm(y32_, T, d, L.ln1_w, L.ln1_b, x32_, xh_, s);
+        end(K_LAYERNORM, s, ev, t * d * 10.0);
+
+        begin(K_GEMM_FFN_UP, s, ev);
+        launch_gemm(L.up, xh_, M, L.b_up, EPI_BIAS_GELU_F16, nullptr, ffn_, s);
+        end(K_GEMM_FFN_UP, s, ev, 2.0 * t * d * f);
+
+        begin(K_GEMM_FFN_DOWN, s, ev);
+        launch_gemm(L.down, ffn_, M, L.b_down, EPI_BIAS_RES_F32, x32_, y32_, s);
+        end(K_GEMM_FFN_DOWN, s, ev, 2.0 * t * d * f);
+
+        begin(K_LAYERNORM, s, ev);
+        launch_layernorm(y32_, T, d, L.ln2_w, L.ln2_b, x32_, xh_, s);
+        end(K_LAYERNORM, s, ev, t * d * 10.0);
+    }
+    begin(K_POOL_L2, s, ev);
+    launch_pool_l2(x32_, d_cu, n_seqs, d, d_out, s);
+    end(K_POOL_L2, s, ev, t * d * 4.0 + (double)n_seqs * d * 4.0);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        std::fprintf(stderr, "libbert: kernel launch failed: %s\n", hipGetErrorString(e));
+        return -1;
+    }
+    return 0;
+}
+
+int Device::forward_host(const int32_t *const *tokens, const int32_t *lens, int n, float *const *out)
+{
+    if (!ok_) return -3;
+    if (n <= 0) return 0;
+    int64_t T = 0;
+    int max_len = 0;
+    for (int i = 0; i < n; ++i) { T += lens[i]; max_len = std::max(max_len, (int)lens[i]); }
+    HIP_RC(hipSetDevice(ordinal_));
+    if (!reserve(T, n)) return -1;
+    h_cu_[0] = 0;
+    for (int i = 0; i < n; ++i) {
+        std::memcpy(h_ids_ + h_cu_[i], tokens[i], sizeof(int32_t) * (size_t)lens[i]);
+        h_cu_[i + 1] = h_cu_[i] + lens[i];
+    }
+    HIP_RC(hipMemcpyAsync(d_ids_, h_ids_, sizeof(int32_t) * (size_t)T, hipMemcpyHostToDevice, stream_));
+    HIP_RC(hipMemcpyAsync(d_cu_, h_cu_, sizeof(int32_t) * (size_t)(n + 1), hipMemcpyHostToDevice, stream_));
+    const int rc = forward(d_ids_, d_cu_, n, max_len, (int)T, d_out_, stream_);
+    if (rc != 0) return rc;
+    const size_t d = (size_t)hp_.n_embd;
+    HIP_RC(hipMemcpyAsync(h_out_, d_out_, sizeof(float) * d * (size_t)n, hipMemcpyDeviceToHost, stream_));
+    HIP_RC(hipStreamSynchronize(stream_));
+    for (int i = 0; i < n; ++i) std::memcpy(out[i], h_out_ + d * (size_t)i, sizeof(float) * d);
+    return 0;
+}
+
+}  // namespace emb
+
+// ---------------------------------------------------------------------------
+// per-kernel parity hook (bert_hip.h): one GEMM on device 0, host buffers
+// ---------------------------------------------------------------------------
+#include "bert_hip.h"
+
+extern "C" int32_t bertx_test_gemm(int32_t fmt, int32_t N, int32_t K, const void *w_rows, const float *bias,
+                                   int32_t M, const uint16_t *x, int32_t epi, const float *res, void *out)
+{
+    using namespace emb;
+    if (!fmt_valid(fmt) || K % 64 || N % 4 || M <= 0 || hip_device_count() == 0) return -1;
+    HostTensor t;
+    t.fmt = fmt; t.ne0 = K; t.ne1 = N;
+    t.bytes.assign((const uint8_t *)w_rows, (const uint8_t *)w_rows + fmt_row_bytes(fmt, K) * (size_t)N);
+    const int fdev = (fmt == FMT_F32 || fmt == FMT_F16) ? FMT_F16 : fmt;
+    Piece q, dd, mm;
+    int n_out = 0, k_out = 0;
+    repack_linear({&t}, fdev, q, dd, mm, n_out, k_out);
+    const int Mp = (int)align_up((size_t)M, GEMM_BM);
+    const size_t osz = epi == EPI_BIAS_RES_F32 ? 4 : 2;
+    char *dq = nullptr, *dd_ = nullptr, *dm = nullptr, *dx = nullptr, *db = nullptr, *dr = nullptr, *dout = nullptr;
+    HIP_RC(hipSetDevice(0));
+    HIP_RC(hipMalloc((void **)&dq, q.bytes.size()));
+    HIP_RC(hipMemcpy(dq, q.bytes.data(), q.bytes.size(), hipMemcpyHostToDevice));
+    if (!dd.bytes.empty()) {
+        HIP_RC(hipMalloc((void **)&dd_, dd.bytes.size()));
+        HIP_RC(hipMemcpy(dd_, dd.bytes.data(), dd.bytes.size(), hipMemcpyHostToDevice));
+    }
+    if (!mm.bytes.empty()) {
+        HIP_RC(hipMalloc((void **)&dm, mm.bytes.size()));
+        HIP_RC(hipMemcpy(dm, mm.bytes.data(), mm.bytes.size(), hipMemcpyHostToDevice));
+    }
+    HIP_RC(hipMalloc((void **)&dx, (size_t)Mp * K * 2));
+    HIP_RC(hipMemset(dx, 0, (size_t)Mp * K * 2));
+    HIP_RC(hipMemcpy(dx, x, (size_t)M * K * 2, hipMemcpyHostToDevice));
+    HIP_RC(hipMalloc((void **)&db, (size_t)N * 4));
+    HIP_RC(hipMemcpy(db, bias, (size_t)N * 4, hipMemcpyHostToDevice));
+    HIP_RC(hipMalloc((void **)&dout, (size_t)Mp * N * osz));
+    if (epi == EPI_BIAS_RES_F32) {
+        HIP_RC(hipMalloc((void **)&dr, (size_t)Mp * N * 4));
+        HIP_RC(hipMemset(dr, 0, (size_t)Mp * N * 4));
+        HIP_RC(hipMemcpy(dr, res, (size_t)M * N * 4, hipMemcpyHostToDevice));
+    }
+    DevWeight W;
+    W.fmt = fdev; W.N = n_out; W.K = k_out;
+    W.qs = dq; W.d = (const uint16_t *)dd_; W.m = (const uint16_t *)dm;
+    launch_gemm(W, (const uint16_t *)dx, Mp, (const float *)db, epi, (const float *)dr, dout, nullptr);
+    HIP_RC(hipGetLastError());
+    HIP_RC(hipDeviceSynchronize());
+    HIP_RC(hipMemcpy(out, dout, (size_t)M * N * osz, hipMemcpyDeviceToHost));
+    for (char *p : {dq, dd_, dm, dx, db, dr, dout}) if (p) (void)hipFree(p);
+    return 0;
+}

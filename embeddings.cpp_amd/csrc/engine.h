@@ -1,0 +1,106 @@
+// Per-GPU engine: one weight replica, one workspace, one stream, one mutex.
+// The forward is the reference's bert_forward_batch graph (bert.cpp:876-1097)
+// as a fixed sequence of HIP launches over a packed (un-padded) token batch.
+#pragma once
+
+#include "host_common.h"
+#include "kernels.h"
+
+#include <hip/hip_runtime.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace emb {
+
+enum KClass : int32_t {
+    K_EMBED_LN = 0, K_GEMM_QKV, K_ATTENTION, K_GEMM_O, K_LAYERNORM, K_GEMM_FFN_UP, K_GEMM_FFN_DOWN, K_POOL_L2,
+    K_NUM_CLASSES
+};
+const char *kclass_name(int k);
+
+struct KStats {
+    int64_t launches = 0;
+    double ms = 0.0;
+    double work = 0.0;     // FLOP (GEMM/attention) or bytes (memory-bound classes)
+};
+
+struct DevLayer {
+    DevWeight qkv, o, up, down;
+    float *b_qkv = nullptr, *b_o = nullptr, *b_up = nullptr, *b_down = nullptr;
+    float *ln1_w = nullptr, *ln1_b = nullptr, *ln2_w = nullptr, *ln2_b = nullptr;
+};
+
+class Device {
+public:
+    Device(int ordinal, const HostModel &m);
+    ~Device();
+    bool ok() const { return ok_; }
+    int ordinal() const { return ordinal_; }
+    hipStream_t stream() const { return stream_; }
+    std::mutex &mutex() { return mu_; }
+
+    // Grow the workspace so one forward of `tokens` packed tokens / `seqs`
+    // sentences fits (never called inside a timed forward).
+    bool reserve(int64_t tokens, int64_t seqs);
+
+    // Device-resident forward (ids, cu, out on this GPU); async on `s`.
+    int forward(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, int max_len, int total_tokens, float *d_out,
+                hipStream_t s);
+
+    // Host-driven forward: packs tokens, H2D, forward, D2H, synchronous.
+    // tokens[i] has lens[i] ids; out[i] receives n_embd floats.
+    int forward_host(const int32_t *const *tokens, const int32_t *lens, int n, float *const *out);
+
+    // profiling
+    void set_profiling(bool on) { profiling_ = on; }
+    void collect_stats();
+    void reset_stats();
+    const KStats &stats(int k) const { return stats_[k]; }
+
+    const HParams &hp() const { return hp_; }
+
+private:
+    struct PendingEv { int cls; hipEvent_t a, b; double work; };
+    void upload(const HostModel &m);
+    void *arena_alloc(size_t bytes);
+    void begin(int cls, hipStream_t s, hipEvent_t &a);
+    void end(int cls, hipStream_t s, hipEvent_t a, double work);
+    hipEvent_t get_event();
+
+    bool ok_ = false;
+    int ordinal_ = 0;
+    HParams hp_;
+    hipStream_t stream_ = nullptr;
+    std::mutex mu_;
+
+    // weights
+    char *arena_ = nullptr;
+    size_t arena_size_ = 0, arena_used_ = 0;
+    DevTable word_, type_, pos_;
+    float *ln_e_w_ = nullptr, *ln_e_b_ = nullptr;
+    std::vector<DevLayer> layers_;
+    int wfmt_ = FMT_F16;
+
+    // workspace
+    int64_t cap_tokens_ = 0, cap_seqs_ = 0;
+    char *ws_ = nullptr;
+    float *x32_ = nullptr, *y32_ = nullptr;
+    uint16_t *xh_ = nullptr, *qkv_ = nullptr, *att_ = nullptr, *ffn_ = nullptr;
+    int32_t *d_ids_ = nullptr, *d_cu_ = nullptr;
+    float *d_out_ = nullptr;
+    int32_t *h_ids_ = nullptr, *h_cu_ = nullptr;   // pinned staging
+    float *h_out_ = nullptr;
+
+    // profiling
+    bool profiling_ = false;
+    std::vector<PendingEv> pending_;
+    std::vector<hipEvent_t> free_events_;
+    KStats stats_[K_NUM_CLASSES];
+};
+
+// HIP device count (0 when no runtime / no GPU); never throws.
+int hip_device_count();
+
+}  // namespace emb

@@ -1,0 +1,70 @@
+// Device-side data layouts and kernel launchers (HIP, gfx950).
+//
+// HBM layout of one model replica (built by engine.cpp at load):
+//   weights  [N][K] linear layers repacked "K-step major" (KS = 64 = two quant
+//            blocks): element (n, k) lives in step ks = k/64 at
+//            ((ks*N + n) * 64 + k%64) -- one K-step of a 128-row tile is one
+//            contiguous, fully coalesced run of bytes.
+//              f16 : 128 B per (ks, n)
+//              q4_0/q4_1: 32 B nibbles per (ks, n) = 2 blocks x 4 words; word w
+//                    of a block holds k = 8w..8w+7 with element e at bit
+//                    4*(e/2) + 16*(e%2) so one AND/OR yields an f16 pair;
+//                    d (and m) f16 [ks][n][2]
+//              q8_0: 64 B per (ks, n), bytes (q ^ 0x80) in order e0 e2 e1 e3 per
+//                    4-group (pair extraction by mask); d f16 [ks][n][2]
+//   QKV      the three projections are one [3d][d] weight (one GEMM, N = 3d)
+//   tables   word/type/pos embeddings in the file's format; q blocks split
+//            into an aligned 16/32 B plane + f16 d (+ m) planes.
+// Activations (per device workspace, rows = packed tokens of all sentences):
+//   X32 [T][d] f32 residual stream, XH [T][d] f16 copy (GEMM input),
+//   QKV [T][3d] f16, ATT [T][d] f16, FFN [T][f] f16, Y32 [T][d] f32.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace emb {
+
+struct DevWeight {
+    int32_t fmt = 0;   // FMT_F16 (also used for f32 files), FMT_Q4_0, FMT_Q4_1, FMT_Q8_0
+    int32_t N = 0, K = 0;
+    const void *qs = nullptr;       // values / nibbles / int8
+    const uint16_t *d = nullptr;    // f16 scales [K/64][N][2]
+    const uint16_t *m = nullptr;    // f16 mins (q4_1)
+};
+
+struct DevTable {
+    int32_t fmt = 0;   // FMT_F32, FMT_F16, FMT_Q4_0, FMT_Q4_1, FMT_Q8_0
+    int32_t rows = 0, cols = 0;
+    const void *qs = nullptr;       // f32/f16 values, or per-block 16 B (q4) / 32 B (q8) planes
+    const uint16_t *d = nullptr;    // [rows][cols/32]
+    const uint16_t *m = nullptr;
+};
+
+enum Epi : int32_t { EPI_BIAS_F16 = 0, EPI_BIAS_GELU_F16 = 1, EPI_BIAS_RES_F32 = 2 };
+
+constexpr int GEMM_BM = 128;          // token rows per tile (M is padded to this)
+constexpr int GEMM_BN = 128;          // output features per tile
+constexpr int ATT_QT = 128;           // queries per attention workgroup
+
+// Y[m][n] = epi( sum_k X[m][k] W[n][k] ), X f16 [M][K] with M % GEMM_BM == 0.
+void launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi,
+                 const float *res, void *out, hipStream_t s);
+
+// x = LN(pos[i] + (type[0] + word[id])) for every valid token (bert.cpp:963-984).
+void launch_embed_ln(const DevTable &word, const DevTable &type, const DevTable &pos, const float *ln_w,
+                     const float *ln_b, const int32_t *ids, const int32_t *cu, int32_t n_seqs, int32_t max_len,
+                     int32_t d, float *x32, uint16_t *xh, hipStream_t s);
+
+// x32 = LN(y), xh = f16(x32) for T rows.
+void launch_layernorm(const float *y, int32_t T, int32_t d, const float *w, const float *b, float *x32,
+                      uint16_t *xh, hipStream_t s);
+
+// Per (sentence, head) softmax(Q K^T / sqrt(dh)) V over the sentence's own keys.
+void launch_attention(const uint16_t *qkv, const int32_t *cu, int32_t n_seqs, int32_t max_len, int32_t n_head,
+                      int32_t d, uint16_t *out, hipStream_t s);
+
+// out[b] = mean_{i<len} x32[start+i] / ||.||  (bert.cpp:1087-1095).
+void launch_pool_l2(const float *x32, const int32_t *cu, int32_t n_seqs, int32_t d, float *out, hipStream_t s);
+
+}  // namespace emb

@@ -1,0 +1,76 @@
+/*
+ * bert_hip.h — MI355X extensions of the bert.h ABI (libbert.so).
+ *
+ * Not part of the reference interface: these entry points exist for callers
+ * that keep their data in HBM (zero-copy integration, bench.py), for live
+ * per-kernel timing, for the native quantizer, and for per-kernel parity
+ * tests.  Plain C types only (no torch / HIP types in the signatures); a
+ * `stream` argument is a hipStream_t passed as void* (NULL = the context's own
+ * stream for that device).
+ */
+#ifndef BERT_HIP_H
+#define BERT_HIP_H
+
+#include "bert.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Number of GPUs the context drives, and the HIP ordinal of slot i. */
+BERT_API int32_t bertx_num_devices(struct bert_ctx *ctx);
+BERT_API int32_t bertx_device_ordinal(struct bert_ctx *ctx, int32_t slot);
+
+/* hparams {n_vocab, n_max_tokens, n_embd, n_intermediate, n_head, n_layer, ftype}. */
+BERT_API void bertx_hparams(struct bert_ctx *ctx, int32_t *out7);
+
+/*
+ * Device-resident forward on GPU `slot`.  d_ids: int32[total_tokens] packed
+ * sentences back to back; d_cu: int32[n_seqs+1] prefix offsets (d_cu[0] = 0,
+ * d_cu[n_seqs] = total_tokens); d_out: float[n_seqs][n_embd].  All three are
+ * device pointers on that GPU.  max_len must be >= every sentence length and
+ * <= n_max_tokens.  Asynchronous on `stream`; returns 0 or a negative error.
+ */
+BERT_API int32_t bertx_forward_device(struct bert_ctx *ctx, int32_t slot,
+                                      const int32_t *d_ids, const int32_t *d_cu,
+                                      int32_t n_seqs, int32_t max_len, int32_t total_tokens,
+                                      float *d_out, void *stream);
+
+/* Make sure the workspace of `slot` can hold total_tokens (so a timed region
+ * never allocates).  Returns 0 or a negative error. */
+BERT_API int32_t bertx_reserve(struct bert_ctx *ctx, int32_t slot, int32_t total_tokens, int32_t n_seqs);
+
+/*
+ * Live kernel timing: when enabled, every launch is bracketed by hipEvents on
+ * its stream and accumulated per kernel class.  bertx_kernel_stats fills the
+ * class name, launch count, summed device milliseconds and summed algorithmic
+ * work (FLOP for GEMM/attention classes, bytes for the memory-bound ones) for
+ * class `idx` (returns 0, or -1 past the last class).  Stats cover launches
+ * whose events have completed (call after a device synchronize).
+ */
+BERT_API void bertx_set_profiling(struct bert_ctx *ctx, int32_t on);
+BERT_API void bertx_reset_stats(struct bert_ctx *ctx);
+BERT_API int32_t bertx_kernel_stats(struct bert_ctx *ctx, int32_t idx, const char **name,
+                                    int64_t *launches, double *total_ms, double *work,
+                                    int32_t *work_is_flops);
+
+/* Native quantizer (mirrors models/quantize.cpp): f32/f16 file -> itype
+ * 2 (q4_0), 3 (q4_1) or 8 (q8_0, extension).  Returns 0 on success. */
+BERT_API int32_t bertx_quantize_file(const char *fname_in, const char *fname_out, int32_t itype);
+
+/*
+ * Per-kernel parity hooks (host buffers in/out, runs synchronously on the
+ * first device).  w_rows: the weight exactly as the model file stores it
+ * (N rows of K elements in format `fmt` = 0,1,2,3,8).  x: f16 bits [M][K].
+ * epi: 0 = +bias -> f16, 1 = +bias, GELU -> f16, 2 = +bias +res(f32) -> f32.
+ */
+BERT_API int32_t bertx_test_gemm(int32_t fmt, int32_t N, int32_t K, const void *w_rows,
+                                 const float *bias, int32_t M, const uint16_t *x,
+                                 int32_t epi, const float *res, void *out);
+
+BERT_API const char *bertx_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BERT_HIP_H */

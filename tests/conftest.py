@@ -1,0 +1,37 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "embeddings.cpp_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); calls the HIP path through the C ABI")
+
+
+@pytest.fixture(scope="session")
+def lib():
+    import bertpy
+    return bertpy.load_lib()
+
+
+@pytest.fixture(scope="session")
+def quant_models(tmp_path_factory):
+    """tiny32/tiny64 in every format: f32/f16 from the reference converter (committed),
+    q4_0/q4_1/q8_0 quantized from the f16 file by the ORACLE quantizer (run_conversions.sh order)."""
+    import oracle_lib
+    d = tmp_path_factory.mktemp("models")
+    out = {}
+    for tiny in ("tiny32", "tiny64"):
+        out[(tiny, "f32")] = os.path.join(GOLDEN, tiny, "ggml-model-f32.bin")
+        out[(tiny, "f16")] = os.path.join(GOLDEN, tiny, "ggml-model-f16.bin")
+        for name, it in (("q4_0", 2), ("q4_1", 3), ("q8_0", 8)):
+            p = str(d / f"{tiny}-{name}.bin")
+            assert oracle_lib.quantize_file(out[(tiny, "f16")], p, it) == 0
+            out[(tiny, name)] = p
+    return out

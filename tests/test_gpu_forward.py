@@ -1,0 +1,120 @@
+"""End-to-end parity of the HIP forward (through the C ABI) with the CPU oracle, the
+committed torch cross-check goldens, and the reference's batching semantics."""
+import os
+
+import numpy as np
+import pytest
+
+import bertpy
+import oracle_lib
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+COS_TOL = 1e-3   # north_star: float vectors within 1e-3 cosine of the reference path
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _one_device():
+    os.environ.pop("BERT_HOST_ONLY", None)
+    os.environ["BERT_DEVICES"] = "0"
+
+
+def ragged_ids(n_vocab, lens, seed=3):
+    rng = np.random.default_rng(seed)
+    return [np.concatenate([[101], rng.integers(104, n_vocab, L - 2), [102]]).astype(np.int32) if L >= 2
+            else np.array([101], np.int32) for L in lens]
+
+
+def cosines(a, b):
+    return np.sum(a * b, axis=1) / (np.linalg.norm(a, axis=1) * np.linalg.norm(b, axis=1))
+
+
+@pytest.mark.parametrize("tiny", ["tiny32", "tiny64"])
+@pytest.mark.parametrize("fmt", ["f32", "f16", "q4_0", "q4_1", "q8_0"])
+def test_forward_matches_oracle(quant_models, tiny, fmt):
+    path = quant_models[(tiny, fmt)]
+    m = bertpy.BertModel(path)
+    o = oracle_lib.Oracle(path)
+    maxl = m.n_max_tokens
+    ids = ragged_ids(o.n_vocab, [2, 3, 17, 64, 100, maxl - 1, maxl, 33])
+    got = m.forward_batch(ids)
+    ref = o.forward_batch(ids)
+    c = cosines(got, ref)
+    assert np.all(c >= 1 - COS_TOL), c
+    assert np.allclose(np.linalg.norm(got, axis=1), 1.0, atol=1e-5)
+
+
+@pytest.mark.parametrize("tiny", ["tiny32", "tiny64"])
+def test_forward_matches_torch_golden(tiny):
+    path = os.path.join(GOLDEN, tiny, "ggml-model-f32.bin")
+    g = np.load(os.path.join(GOLDEN, tiny, "forward_f32.npz"))
+    lens = g["lens"]
+    offs = np.concatenate([[0], np.cumsum(lens)])
+    ids = [g["ids"][offs[i]:offs[i + 1]] for i in range(len(lens))]
+    got = bertpy.BertModel(path).forward_batch(ids)
+    assert np.all(cosines(got, g["torch_emb"]) >= 1 - COS_TOL)
+    assert np.all(cosines(got, g["oracle_emb"]) >= 1 - COS_TOL)
+
+
+def test_batch_composition_invariance(quant_models):
+    """A sentence's embedding must not depend on what else is in the batch (bitwise)."""
+    m = bertpy.BertModel(quant_models[("tiny64", "q4_0")])
+    ids = ragged_ids(690, [5, 300, 512, 40, 2, 129])
+    full = m.forward_batch(ids)
+    for i in (0, 2, 4):
+        alone = m.forward_batch([ids[i]])
+        assert np.array_equal(alone[0], full[i])
+    rev = m.forward_batch(ids[::-1])
+    assert np.array_equal(rev[::-1], full)
+
+
+def test_fake_batch_and_forward(quant_models):
+    m = bertpy.BertModel(quant_models[("tiny32", "f16")])
+    ids = ragged_ids(690, [4, 50, 128])
+    a = m.forward_batch(ids)
+    b = m.forward_batch(ids, fake=True)
+    assert np.all(cosines(a, b) >= 1 - 1e-6)
+    one = m.forward(ids[1])
+    assert np.all(cosines(one[None], a[1:2]) >= 1 - 1e-6)
+
+
+def test_too_long_is_refused(quant_models):
+    m = bertpy.BertModel(quant_models[("tiny32", "f16")])
+    ids = ragged_ids(690, [10, 129])          # n_max_tokens = 128
+    out = m.forward_batch(ids, fill=5.0)
+    assert np.all(out == 5.0)                 # bert.cpp:867-871: nothing written
+    fake = m.forward_batch(ids, fake=True, fill=5.0)
+    assert not np.all(fake[0] == 5.0) and np.all(fake[1] == 5.0)   # stops at the first long input
+
+
+def test_encode_batch_matches_oracle(quant_models):
+    import json
+    path = quant_models[("tiny64", "q8_0")]
+    m = bertpy.BertModel(path)
+    o = oracle_lib.Oracle(path)
+    cases = json.load(open(os.path.join(GOLDEN, "tokenizer_cases.json")))["cases"]
+    texts = [bytes.fromhex(c["text_hex"]) for c in cases if c["n_max_tokens"] == 512][:60]
+    for bs in (len(texts), 16, 7, 1):
+        got = m.encode(texts, batch_size=bs)
+        ref, written = o.encode_batch(texts, bs)
+        wrote = ~np.all(got == 0.0, axis=1)
+        assert np.array_equal(wrote, written), bs
+        c = cosines(got[written], ref[written])
+        assert np.all(c >= 1 - COS_TOL), (bs, c.min())
+
+
+def test_bge_base_q4_0_full_size(tmp_path):
+    """BASELINE config shape: bge-base q4_0, L = 512, B = 64.  Oracle parity on two
+    sentences; size-independent properties on the full batch."""
+    path = str(tmp_path / "bge-base-q4_0.bin")
+    bertpy.synthetic_model(path, "bge-base-en-v1.5", "q4_0", seed=1234)
+    m = bertpy.BertModel(path)
+    ids = bertpy.synthetic_ids(64, 512, 30522, seed=7)
+    full = m.forward_batch(ids)
+    assert np.all(np.isfinite(full))
+    assert np.allclose(np.linalg.norm(full, axis=1), 1.0, atol=1e-5)
+    two = m.forward_batch(ids[:2])
+    assert np.array_equal(two, full[:2])
+    ref = oracle_lib.Oracle(path).forward_batch(ids[:2], n_threads=min(16, os.cpu_count() or 1))
+    assert np.all(cosines(full[:2], ref) >= 1 - COS_TOL)

@@ -1,0 +1,83 @@
+"""Per-kernel parity on the GPU: the fused dequant GEMM (bertx_test_gemm) against a numpy
+fp32/f64 reference of the same op, for every weight format and epilogue."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle_lib
+
+pytestmark = pytest.mark.gpu
+
+FMTS = {0: "f32", 1: "f16", 2: "q4_0", 3: "q4_1", 8: "q8_0"}
+BLOCK = {2: 18, 3: 20, 8: 34}
+
+
+def weight_rows(fmt, W):
+    """File-format bytes of W [N][K] and its dequantized f32 values (oracle dequantizer)."""
+    N, K = W.shape
+    if fmt == 0:
+        return W.astype(np.float32).tobytes(), W.astype(np.float32)
+    if fmt == 1:
+        h = W.astype(np.float16)
+        return h.tobytes(), h.astype(np.float32)
+    L = oracle_lib.lib()
+    rows = []
+    deq = np.zeros((N, K), np.float32)
+    for n in range(N):
+        buf = ctypes.create_string_buffer(K // 32 * BLOCK[fmt])
+        x = np.ascontiguousarray(W[n], np.float32)
+        L.oracle_quantize_row(fmt, x.ctypes.data, buf, K)
+        L.oracle_dequantize_row(fmt, buf, deq[n].ctypes.data, K)
+        rows.append(buf.raw)
+    return b"".join(rows), deq
+
+
+def run_gemm(lib, fmt, W, bias, X, epi, res=None):
+    N, K = W.shape
+    M = X.shape[0]
+    wb, deq = weight_rows(fmt, W)
+    xh = np.ascontiguousarray(X.astype(np.float16))
+    out = np.zeros((M, N), np.float32 if epi == 2 else np.float16)
+    resp = None
+    if epi == 2:
+        res = np.ascontiguousarray(res, np.float32)
+        resp = res.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+    rc = lib.bertx_test_gemm(fmt, N, K, wb, np.ascontiguousarray(bias, np.float32).ctypes.data_as(
+        ctypes.POINTER(ctypes.c_float)), M, xh.ctypes.data, epi, resp, out.ctypes.data)
+    assert rc == 0
+    return out.astype(np.float32), deq, xh.astype(np.float32)
+
+
+@pytest.mark.parametrize("fmt", sorted(FMTS))
+@pytest.mark.parametrize("epi", [0, 1, 2])
+@pytest.mark.parametrize("shape", [(192, 256, 300), (768, 768, 512)])
+def test_gemm_matches_numpy(lib, fmt, epi, shape):
+    N, K, M = shape
+    rng = np.random.default_rng(fmt * 10 + epi)
+    W = rng.standard_normal((N, K)).astype(np.float32) * 0.05
+    W[:, 5] *= 20.0                       # asymmetric outliers catch transposed maps
+    bias = rng.standard_normal(N).astype(np.float32) * 0.1
+    X = rng.standard_normal((M, K)).astype(np.float32)
+    X[7] *= 3.0
+    res = rng.standard_normal((M, N)).astype(np.float32) if epi == 2 else None
+    got, deq, xh = run_gemm(lib, fmt, W, bias, X, epi, res)
+    # the kernel multiplies f16 operands with f32 accumulation: reference uses f16(weights)
+    wref = deq.astype(np.float16).astype(np.float64)
+    acc = xh.astype(np.float64) @ wref.T + bias.astype(np.float64)
+    if epi == 0:
+        ref = acc
+        tol = 2e-3 * np.abs(ref).max()
+    elif epi == 1:
+        x16 = acc.astype(np.float16).astype(np.float64)
+        ref = 0.5 * x16 * (1 + np.tanh(0.7978845608028654 * x16 * (1 + 0.044715 * x16 * x16)))
+        tol = 3e-3 * np.abs(ref).max()
+    else:
+        ref = res.astype(np.float64) + acc
+        tol = 2e-5 * np.abs(ref).max() * np.sqrt(K / 64)
+    err = np.abs(got - ref).max()
+    assert err <= tol, (FMTS[fmt], epi, err, tol)
+    # and the dequantized value itself is what the reference uses (f32 math)
+    exact = xh.astype(np.float64) @ deq.astype(np.float64).T + bias
+    if epi == 0:
+        assert np.abs(got - exact).max() <= 5e-3 * np.abs(exact).max()
