@@ -1,0 +1,151 @@
+// Flash-style self-attention for gfx950 (reference bert.cpp:1018-1036).
+#include "device_common.h"
+#include "kernels.h"
+
+#include <cmath>
+
+namespace emb {
+
+// ---------------------------------------------------------------------------
+// attention: flash-style, one workgroup = 128 queries of one (sentence, head),
+// 4 waves x 32 queries.  S^T = K Q^T per 32-key block (query on the lane,
+// keys in registers) -> online softmax in registers -> O^T += V^T P^T with
+// the S accumulator reused as the B operand (no LDS round trip for P).
+// Keys past the sentence end get probability exactly 0, as the reference's
+// -1e5 mask does after its fp16 exp (bert.cpp:957-961, 1024-1025).
+// ---------------------------------------------------------------------------
+
+template <int DH>
+__global__ __launch_bounds__(256) void attention_kernel(const h16 *__restrict__ qkv, const int32_t *__restrict__ cu,
+                                                        int d, float sl2, h16 *__restrict__ out)
+{
+    constexpr int KT = 64, KSTR = DH + 8, VSTR = KT + 8;
+    __shared__ __attribute__((aligned(16))) h16 Ks[KT * KSTR];
+    __shared__ __attribute__((aligned(16))) h16 Vt[DH * VSTR];
+    const int b = blockIdx.z, h = blockIdx.y;
+    const int start = cu[b], len = cu[b + 1] - start;
+    const int q0 = blockIdx.x * ATT_QT;
+    if (q0 >= len) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int hi = lane >> 5, lq = lane & 31;
+    const int ld = 3 * d;
+    const int q = q0 + w * 32 + lq;
+
+    h16x8 qf[DH / 16];
+    const h16 *qrow = qkv + (size_t)(start + q) * ld + h * DH;
+#pragma unroll
+    for (int s = 0; s < DH / 16; ++s) qf[s] = *(const h16x8 *)(qrow + 16 * s + 8 * hi);
+
+    f32x16 o[DH / 32];
+#pragma unroll
+    for (int t = 0; t < DH / 32; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[t][r] = 0.f;
+    float m_i = -INFINITY, l_i = 0.f;
+
+    const int nkt = (len + KT - 1) / KT;
+    for (int kt = 0; kt < nkt; ++kt) {
+        const int k0 = kt * KT;
+        __syncthreads();
+        // K tile row-major (coalesced: chunk index fastest)
+        for (int c = tid; c < KT * DH / 8; c += 256) {
+            const int r = c / (DH / 8), ch = c % (DH / 8);
+            *(uint4 *)(Ks + r * KSTR + ch * 8) = *(const uint4 *)(qkv + (size_t)(start + k0 + r) * ld + d + h * DH + ch * 8);
+        }
+        // V tile transposed into Vt[d][key] (key fastest across lanes: conflict-free 2-byte writes)
+        for (int c = tid; c < KT * DH / 8; c += 256) {
+            const int r = c % KT, ch = c / KT;
+            const h16x8 vv = *(const h16x8 *)(qkv + (size_t)(start + k0 + r) * ld + 2 * d + h * DH + ch * 8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) Vt[(ch * 8 + e) * VSTR + r] = vv[e];
+        }
+        __syncthreads();
+
+        f32x16 s[2];
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[kh][r] = 0.f;
+#pragma unroll
+            for (int st = 0; st < DH / 16; ++st) {
+                const h16x8 a = *(const h16x8 *)(Ks + (kh * 32 + lq) * KSTR + 16 * st + 8 * hi);
+                s[kh] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, qf[st], s[kh], 0, 0, 0);
+            }
+        }
+        float mx = -INFINITY;
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int key = k0 + kh * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+                const float v = key < len ? s[kh][r] * sl2 : -INFINITY;
+                s[kh][r] = v;
+                mx = fmaxf(mx, v);
+            }
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float m_new = fmaxf(m_i, mx);
+        const float alpha = exp2f(m_i - m_new);
+        float rs = 0.f;
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float p = exp2f(s[kh][r] - m_new);
+                s[kh][r] = p;
+                rs += p;
+            }
+        rs += __shfl_xor(rs, 32, 64);
+        l_i = l_i * alpha + rs;
+        m_i = m_new;
+#pragma unroll
+        for (int t = 0; t < DH / 32; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) {
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                h16x8 bp;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) bp[j] = (h16)s[kh][8 * s2 + j];
+#pragma unroll
+                for (int t = 0; t < DH / 32; ++t) {
+                    const h16 *vr = Vt + (32 * t + lq) * VSTR + 32 * kh + 16 * s2 + 4 * hi;
+                    const h16x4 lo = *(const h16x4 *)vr;
+                    const h16x4 up = *(const h16x4 *)(vr + 8);
+                    const h16x8 a = {lo[0], lo[1], lo[2], lo[3], up[0], up[1], up[2], up[3]};
+                    o[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bp, o[t], 0, 0, 0);
+                }
+            }
+        }
+    }
+
+    if (q < len) {
+        const float inv = 1.0f / l_i;
+        h16 *orow = out + (size_t)(start + q) * d + h * DH;
+#pragma unroll
+        for (int t = 0; t < DH / 32; ++t)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                h16x4 v;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = (h16)(o[t][4 * g + e] * inv);
+                *(h16x4 *)(orow + 32 * t + 8 * g + 4 * hi) = v;
+            }
+    }
+}
+
+void launch_attention(const uint16_t *qkv, const int32_t *cu, int32_t n_seqs, int32_t max_len, int32_t n_head,
+                      int32_t d, uint16_t *out, hipStream_t s)
+{
+    const int dh = d / n_head;
+    const float sl2 = (1.0f / sqrtf((float)dh)) * 1.4426950408889634f;
+    dim3 grid((max_len + ATT_QT - 1) / ATT_QT, n_head, n_seqs);
+    if (dh == 64)
+        attention_kernel<64><<<grid, 256, 0, s>>>((const h16 *)qkv, cu, d, sl2, (h16 *)out);
+    else
+        attention_kernel<32><<<grid, 256, 0, s>>>((const h16 *)qkv, cu, d, sl2, (h16 *)out);
+}
+
+}  // namespace emb

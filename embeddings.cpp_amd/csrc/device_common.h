@@ -1,0 +1,61 @@
+// Device-side helpers shared by the gfx950 kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace emb {
+
+typedef _Float16 h16;
+typedef h16 h16x8 __attribute__((ext_vector_type(8)));
+typedef h16 h16x4 __attribute__((ext_vector_type(4)));
+typedef h16 h16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+__device__ __forceinline__ float wave_sum(float v)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ h16x2 as_h2(uint32_t u) { return __builtin_bit_cast(h16x2, u); }
+__device__ __forceinline__ h16 as_h(uint16_t u) { return __builtin_bit_cast(h16, u); }
+
+// ggml-era GELU (tanh form) on an f16-rounded input, result rounded to f16 --
+// the value ggml's GGML_GELU_FP16 table holds (bert.cpp:1063).  Evaluated as
+// 0.5 x (1 + tanh(u)) = x / (1 + exp(-2u)), well inside f16 rounding.
+__device__ __forceinline__ h16 gelu_era(float v)
+{
+    const float x = (float)(h16)v;
+    const float u2 = -2.0f * 1.4426950408889634f * 0.79788456080286535587989211986876f;   // -2 log2(e) sqrt(2/pi)
+    const float e = __builtin_amdgcn_exp2f(u2 * x * (1.0f + 0.044715f * x * x));
+    return (h16)(x * __builtin_amdgcn_rcpf(1.0f + e));
+}
+
+// LDS-DMA: `size` bytes per lane from the per-lane global address `g` into
+// LDS at (wave-uniform) `lds_base` + lane * size.
+template <int SIZE>
+__device__ __forceinline__ void glds(const void *g, void *lds_base)
+{
+    static_assert(SIZE == 4 || SIZE == 16, "LDS-DMA widths used here");
+    if constexpr (SIZE == 16) __builtin_amdgcn_global_load_lds(g, (lds_void_t *)lds_base, 16, 0, 0);
+    else __builtin_amdgcn_global_load_lds(g, (lds_void_t *)lds_base, 4, 0, 0);
+}
+
+__device__ __forceinline__ void lds_barrier()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt()
+{
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+}  // namespace emb

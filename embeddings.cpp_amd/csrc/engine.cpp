@@ -282,6 +282,7 @@ bool Device::reserve(int64_t tokens, int64_t seqs)
     const size_t o_x32 = take(rows * d * 4), o_y32 = take(rows * d * 4), o_xh = take(rows * d * 2);
     const size_t o_qkv = take(rows * 3 * d * 2), o_att = take(rows * d * 2), o_ffn = take(rows * f * 2);
     const size_t o_ids = take(rows * 4), o_cu = take((ns + 1) * 4), o_out = take(ns * d * 4);
+    const size_t o_pool = take((size_t)ns * pool_chunks(hp_.n_max_tokens) * d * 4);
     if (ws_) { (void)hipFree(ws_); ws_ = nullptr; }
     if (h_ids_) { (void)hipHostFree(h_ids_); h_ids_ = nullptr; }
     if (h_cu_) { (void)hipHostFree(h_cu_); h_cu_ = nullptr; }
@@ -292,6 +293,7 @@ bool Device::reserve(int64_t tokens, int64_t seqs)
     x32_ = (float *)(ws_ + o_x32); y32_ = (float *)(ws_ + o_y32); xh_ = (uint16_t *)(ws_ + o_xh);
     qkv_ = (uint16_t *)(ws_ + o_qkv); att_ = (uint16_t *)(ws_ + o_att); ffn_ = (uint16_t *)(ws_ + o_ffn);
     d_ids_ = (int32_t *)(ws_ + o_ids); d_cu_ = (int32_t *)(ws_ + o_cu); d_out_ = (float *)(ws_ + o_out);
+    pool_part_ = (float *)(ws_ + o_pool);
     HIP_OK(hipHostMalloc((void **)&h_ids_, nt * 4, hipHostMallocDefault));
     HIP_OK(hipHostMalloc((void **)&h_cu_, (ns + 1) * 4, hipHostMallocDefault));
     HIP_OK(hipHostMalloc((void **)&h_out_, ns * d * 4, hipHostMallocDefault));
@@ -395,7 +397,7 @@ int Device::forward(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, int m
         end(K_LAYERNORM, s, ev, t * d * 10.0);
     }
     begin(K_POOL_L2, s, ev);
-    launch_pool_l2(x32_, d_cu, n_seqs, d, d_out, s);
+    launch_pool_l2(x32_, d_cu, n_seqs, max_len, d, pool_part_, d_out, s);
     end(K_POOL_L2, s, ev, t * d * 4.0 + (double)n_seqs * d * 4.0);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
@@ -438,7 +440,8 @@ int Device::forward_host(const int32_t *const *tokens, const int32_t *lens, int 
 #include "bert_hip.h"
 
 extern "C" int32_t bertx_test_gemm(int32_t fmt, int32_t N, int32_t K, const void *w_rows, const float *bias,
-                                   int32_t M, const uint16_t *x, int32_t epi, const float *res, void *out)
+                                   int32_t M, const uint16_t *x, int32_t epi, const float *res, void *out,
+                                   int32_t tile_n)
 {
     using namespace emb;
     if (!fmt_valid(fmt) || K % 64 || N % 4 || M <= 0 || hip_device_count() == 0) return -1;
@@ -477,7 +480,9 @@ extern "C" int32_t bertx_test_gemm(int32_t fmt, int32_t N, int32_t K, const void
     DevWeight W;
     W.fmt = fdev; W.N = n_out; W.K = k_out;
     W.qs = dq; W.d = (const uint16_t *)dd_; W.m = (const uint16_t *)dm;
+    g_force_bn = tile_n;
     launch_gemm(W, (const uint16_t *)dx, Mp, (const float *)db, epi, (const float *)dr, dout, nullptr);
+    g_force_bn = 0;
     HIP_RC(hipGetLastError());
     HIP_RC(hipDeviceSynchronize());
     HIP_RC(hipMemcpy(out, dout, (size_t)M * N * osz, hipMemcpyDeviceToHost));

@@ -90,6 +90,7 @@ private:
     uint16_t *xh_ = nullptr, *qkv_ = nullptr, *att_ = nullptr, *ffn_ = nullptr;
     int32_t *d_ids_ = nullptr, *d_cu_ = nullptr;
     float *d_out_ = nullptr;
+    float *pool_part_ = nullptr;
     int32_t *h_ids_ = nullptr, *h_cu_ = nullptr;   // pinned staging
     float *h_out_ = nullptr;
 

@@ -43,13 +43,16 @@ struct DevTable {
 
 enum Epi : int32_t { EPI_BIAS_F16 = 0, EPI_BIAS_GELU_F16 = 1, EPI_BIAS_RES_F32 = 2 };
 
-constexpr int GEMM_BM = 128;          // token rows per tile (M is padded to this)
+constexpr int GEMM_BM = 256;          // token rows per tile (M is padded to this)
 constexpr int GEMM_BN = 128;          // output features per tile
 constexpr int ATT_QT = 128;           // queries per attention workgroup
 
 // Y[m][n] = epi( sum_k X[m][k] W[n][k] ), X f16 [M][K] with M % GEMM_BM == 0.
 void launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi,
                  const float *res, void *out, hipStream_t s);
+
+// Tests only: force the GEMM tile width (128 / 256; 0 = heuristic).
+extern int g_force_bn;
 
 // x = LN(pos[i] + (type[0] + word[id])) for every valid token (bert.cpp:963-984).
 void launch_embed_ln(const DevTable &word, const DevTable &type, const DevTable &pos, const float *ln_w,
@@ -65,6 +68,10 @@ void launch_attention(const uint16_t *qkv, const int32_t *cu, int32_t n_seqs, in
                       int32_t d, uint16_t *out, hipStream_t s);
 
 // out[b] = mean_{i<len} x32[start+i] / ||.||  (bert.cpp:1087-1095).
-void launch_pool_l2(const float *x32, const int32_t *cu, int32_t n_seqs, int32_t d, float *out, hipStream_t s);
+// Two stages: per-64-token-chunk partial sums into partial[n_seqs][pool_chunks][d],
+// then sum + normalise.
+int32_t pool_chunks(int32_t max_len);
+void launch_pool_l2(const float *x32, const int32_t *cu, int32_t n_seqs, int32_t max_len, int32_t d, float *partial,
+                    float *out, hipStream_t s);
 
 }  // namespace emb

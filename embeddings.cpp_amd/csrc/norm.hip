@@ -1,0 +1,201 @@
+// Memory-bound row kernels: embeddings + LayerNorm, LayerNorm, mean pool + L2.
+// One wave per token row; each lane owns 4 consecutive features per 256-wide
+// slice (16-B loads and stores), reductions by wave shuffles.
+#include "device_common.h"
+#include "host_common.h"
+#include "kernels.h"
+
+#include <cmath>
+
+namespace emb {
+
+namespace {
+
+constexpr int MAXV = 4;   // 4 slices x 256 features = n_embd <= 1024
+
+// 4 consecutive table values starting at column c (c % 4 == 0)
+__device__ __forceinline__ f32x4 table4(const DevTable &t, int row, int c)
+{
+    f32x4 r;
+    switch (t.fmt) {
+    case FMT_F32: return *(const f32x4 *)((const float *)t.qs + (size_t)row * t.cols + c);
+    case FMT_F16: {
+        const h16x4 h = *(const h16x4 *)((const h16 *)t.qs + (size_t)row * t.cols + c);
+        r[0] = h[0]; r[1] = h[1]; r[2] = h[2]; r[3] = h[3];
+        return r;
+    }
+    case FMT_Q8_0: {
+        const size_t b = (size_t)row * (t.cols / 32) + c / 32;
+        const uint32_t w = *(const uint32_t *)((const int8_t *)t.qs + b * 32 + (c & 31));
+        const float d = (float)as_h(t.d[b]);
+        r[0] = (float)(int8_t)(w & 0xff) * d; r[1] = (float)(int8_t)((w >> 8) & 0xff) * d;
+        r[2] = (float)(int8_t)((w >> 16) & 0xff) * d; r[3] = (float)(int8_t)(w >> 24) * d;
+        return r;
+    }
+    default: {   // q4_0 / q4_1, file nibble order: element j<16 low nibble of byte j, j>=16 high of j-16
+        const size_t b = (size_t)row * (t.cols / 32) + c / 32;
+        const int j = c & 31;
+        const uint32_t w = *(const uint32_t *)((const uint8_t *)t.qs + b * 16 + (j & 15));
+        const int sh = j < 16 ? 0 : 4;
+        const float d = (float)as_h(t.d[b]);
+        const float mn = t.fmt == FMT_Q4_1 ? (float)as_h(t.m[b]) : 0.0f;
+        const int o = t.fmt == FMT_Q4_1 ? 0 : 8;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int q = (int)((w >> (8 * e + sh)) & 15u) - o;
+            r[e] = t.fmt == FMT_Q4_1 ? (float)q * d + mn : (float)q * d;
+        }
+        return r;
+    }
+    }
+}
+
+// ggml_norm (eps 1e-5, mean then centred variance) * w + b, bert.cpp:977-984
+__device__ __forceinline__ void ln_row(f32x4 (&v)[MAXV], int d, int lane, const float *w, const float *b, float *x32,
+                                       h16 *xh)
+{
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+        const int c = 4 * (lane + 64 * k);
+        if (c < d) s += (v[k][0] + v[k][1]) + (v[k][2] + v[k][3]);
+    }
+    const float mean = wave_sum(s) / (float)d;
+    float s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+        const int c = 4 * (lane + 64 * k);
+        if (c < d) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { v[k][e] -= mean; s2 += v[k][e] * v[k][e]; }
+        }
+    }
+    const float scale = 1.0f / sqrtf(wave_sum(s2) / (float)d + 1e-5f);
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+        const int c = 4 * (lane + 64 * k);
+        if (c >= d) continue;
+        const f32x4 ww = *(const f32x4 *)(w + c), bb = *(const f32x4 *)(b + c);
+        f32x4 y;
+        h16x4 yh;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { y[e] = ww[e] * (v[k][e] * scale) + bb[e]; yh[e] = (h16)y[e]; }
+        *(f32x4 *)(x32 + c) = y;
+        *(h16x4 *)(xh + c) = yh;
+    }
+}
+
+__global__ __launch_bounds__(256) void embed_ln_kernel(DevTable word, DevTable type, DevTable pos,
+                                                       const float *__restrict__ ln_w, const float *__restrict__ ln_b,
+                                                       const int32_t *__restrict__ ids, const int32_t *__restrict__ cu,
+                                                       int d, float *__restrict__ x32, h16 *__restrict__ xh)
+{
+    const int b = blockIdx.y, lane = threadIdx.x & 63;
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int start = cu[b], len = cu[b + 1] - start;
+    if (i >= len) return;
+    const int t = start + i, id = ids[t];
+    f32x4 v[MAXV];
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+        const int c = 4 * (lane + 64 * k);
+        if (c < d) {
+            // pos + (type[0] + word[id])  (bert.cpp:968-973 operand order)
+            const f32x4 w = table4(word, id, c), ty = table4(type, 0, c), p = table4(pos, i, c);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[k][e] = p[e] + (ty[e] + w[e]);
+        }
+    }
+    ln_row(v, d, lane, ln_w, ln_b, x32 + (size_t)t * d, xh + (size_t)t * d);
+}
+
+__global__ __launch_bounds__(256) void layernorm_kernel(const float *__restrict__ y, int T, int d,
+                                                        const float *__restrict__ w, const float *__restrict__ b,
+                                                        float *__restrict__ x32, h16 *__restrict__ xh)
+{
+    const int lane = threadIdx.x & 63;
+    const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (t >= T) return;
+    f32x4 v[MAXV];
+    const float *row = y + (size_t)t * d;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+        const int c = 4 * (lane + 64 * k);
+        if (c < d) v[k] = *(const f32x4 *)(row + c);
+    }
+    ln_row(v, d, lane, w, b, x32 + (size_t)t * d, xh + (size_t)t * d);
+}
+
+// pool stage 1: partial column sums of 64-token chunks, weights 1/len
+// (bert.cpp:1087-1089: sum_i X[i][c] * (1/len)).
+constexpr int POOL_CHUNK = 64;
+
+__global__ __launch_bounds__(256) void pool_partial_kernel(const float *__restrict__ x32, const int32_t *__restrict__ cu,
+                                                           int d, int n_chunks, float *__restrict__ part)
+{
+    const int b = blockIdx.y, ch = blockIdx.x;
+    const int start = cu[b], len = cu[b + 1] - start;
+    const int i0 = ch * POOL_CHUNK;
+    float *dst = part + ((size_t)b * n_chunks + ch) * d;
+    const float wt = 1.0f / (float)len;
+    for (int c = 4 * threadIdx.x; c < d; c += 4 * 256) {
+        f32x4 a = {0.f, 0.f, 0.f, 0.f};
+        const int i1 = min(len, i0 + POOL_CHUNK);
+        for (int i = i0; i < i1; ++i) {
+            const f32x4 x = *(const f32x4 *)(x32 + (size_t)(start + i) * d + c);
+            a[0] += x[0] * wt; a[1] += x[1] * wt; a[2] += x[2] * wt; a[3] += x[3] * wt;
+        }
+        *(f32x4 *)(dst + c) = a;
+    }
+}
+
+// pool stage 2: sum the chunks, divide by the L2 norm (bert.cpp:1092-1095)
+__global__ __launch_bounds__(256) void pool_final_kernel(const float *__restrict__ part, int d, int n_chunks,
+                                                         float *__restrict__ out)
+{
+    __shared__ float red[4];
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    float e[4];
+    float ss = 0.f;
+    int ne = 0;
+    for (int c = tid; c < d; c += 256) {
+        float v = 0.f;
+        for (int k = 0; k < n_chunks; ++k) v += part[((size_t)b * n_chunks + k) * d + c];
+        e[ne++] = v;
+        ss += v * v;
+    }
+    ss = wave_sum(ss);
+    if (lane == 0) red[w] = ss;
+    __syncthreads();
+    const float nrm = sqrtf((red[0] + red[1]) + (red[2] + red[3]));
+    ne = 0;
+    for (int c = tid; c < d; c += 256) out[(size_t)b * d + c] = e[ne++] / nrm;
+}
+
+}  // namespace
+
+void launch_embed_ln(const DevTable &word, const DevTable &type, const DevTable &pos, const float *ln_w,
+                     const float *ln_b, const int32_t *ids, const int32_t *cu, int32_t n_seqs, int32_t max_len,
+                     int32_t d, float *x32, uint16_t *xh, hipStream_t s)
+{
+    dim3 grid((max_len + 3) / 4, n_seqs);
+    embed_ln_kernel<<<grid, 256, 0, s>>>(word, type, pos, ln_w, ln_b, ids, cu, d, x32, (h16 *)xh);
+}
+
+void launch_layernorm(const float *y, int32_t T, int32_t d, const float *w, const float *b, float *x32,
+                      uint16_t *xh, hipStream_t s)
+{
+    layernorm_kernel<<<(T + 3) / 4, 256, 0, s>>>(y, T, d, w, b, x32, (h16 *)xh);
+}
+
+int32_t pool_chunks(int32_t max_len) { return (max_len + POOL_CHUNK - 1) / POOL_CHUNK; }
+
+void launch_pool_l2(const float *x32, const int32_t *cu, int32_t n_seqs, int32_t max_len, int32_t d, float *partial,
+                    float *out, hipStream_t s)
+{
+    const int nc = pool_chunks(max_len);
+    pool_partial_kernel<<<dim3(nc, n_seqs), 256, 0, s>>>(x32, cu, d, nc, partial);
+    pool_final_kernel<<<n_seqs, 256, 0, s>>>(partial, d, nc, out);
+}
+
+}  // namespace emb
