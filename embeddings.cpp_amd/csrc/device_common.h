@@ -52,10 +52,17 @@ __device__ __forceinline__ void lds_barrier()
     asm volatile("" ::: "memory");
 }
 
+// s_waitcnt vmcnt(N) through the builtin (not inline asm) so the compiler's
+// waitcnt pass knows the loads older than the N youngest have retired and does
+// not add its own conservative vmcnt(0) at their first use.  gfx9 encoding:
+// vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt_hi[15:14]; other counters
+// left at their maximum (no wait).
 template <int N>
 __device__ __forceinline__ void wait_vmcnt()
 {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+    asm volatile("" ::: "memory");
 }
 
 }  // namespace emb

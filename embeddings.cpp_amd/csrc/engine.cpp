@@ -100,25 +100,25 @@ void repack_linear(const std::vector<const HostTensor *> &parts, int fmt_dev, Pi
                 const size_t di = ((size_t)(b / 2) * N + n) * 2 + (b & 1);
                 (void)KS;
                 std::memcpy(&dd[di], blk, 2);
+                // element e of block b lands at k-slice kk = 2*(b&1) + e/16, lane half
+                // h = (e/8)&1, position i = e%8 of that (kk, h) fragment (kernels.h)
+                const size_t rec = (size_t)(b / 2) * N + n;
                 if (fmt_dev == FMT_Q8_0) {
                     const int8_t *q = (const int8_t *)(blk + 2);
-                    uint8_t *o = qs.bytes.data() + di * 32;
-                    for (int g = 0; g < 8; ++g) {
-                        const int order[4] = {0, 2, 1, 3};
-                        for (int i = 0; i < 4; ++i) o[4 * g + i] = (uint8_t)((uint8_t)q[4 * g + order[i]] ^ 0x80u);
+                    uint8_t *o = qs.bytes.data() + rec * 64;
+                    static const int pos4[4] = {0, 2, 1, 3};
+                    for (int e = 0; e < 32; ++e) {
+                        const int kk = 2 * (b & 1) + e / 16, h = (e / 8) & 1, i = e % 8;
+                        o[32 * h + 8 * kk + 4 * (i / 4) + pos4[i % 4]] = (uint8_t)((uint8_t)q[e] ^ 0x80u);
                     }
                 } else {
                     const uint8_t *nib = blk + (fmt_dev == FMT_Q4_1 ? 4 : 2);
                     if (mm) std::memcpy(&mm[di], blk + 2, 2);
-                    uint32_t *o = (uint32_t *)(qs.bytes.data() + di * 16);
-                    for (int w = 0; w < 4; ++w) {
-                        uint32_t word = 0;
-                        for (int i = 0; i < 8; ++i) {
-                            const int e = 8 * w + i;
-                            const uint32_t q = e < 16 ? (nib[e] & 15u) : (uint32_t)(nib[e - 16] >> 4);
-                            word |= q << (4 * (i / 2) + 16 * (i % 2));
-                        }
-                        o[w] = word;
+                    uint32_t *o = (uint32_t *)(qs.bytes.data() + rec * 32);
+                    for (int e = 0; e < 32; ++e) {
+                        const int kk = 2 * (b & 1) + e / 16, h = (e / 8) & 1, i = e % 8;
+                        const uint32_t q = e < 16 ? (nib[e] & 15u) : (uint32_t)(nib[e - 16] >> 4);
+                        o[4 * h + kk] |= q << (4 * (i / 2) + 16 * (i % 2));
                     }
                 }
             }
@@ -488,4 +488,68 @@ extern "C" int32_t bertx_test_gemm(int32_t fmt, int32_t N, int32_t K, const void
     HIP_RC(hipMemcpy(out, dout, (size_t)M * N * osz, hipMemcpyDeviceToHost));
     for (char *p : {dq, dd_, dm, dx, db, dr, dout}) if (p) (void)hipFree(p);
     return 0;
+}
+
+// ---------------------------------------------------------------------------
+// GEMM micro-benchmark (bert_hip.h): device-timed launches on random operands
+// ---------------------------------------------------------------------------
+extern "C" int32_t bertx_bench_gemm(int32_t fmt, int32_t N, int32_t K, int32_t M, int32_t epi, int32_t tile_n,
+                                    int32_t ablate, int32_t iters, float *avg_us)
+{
+    using namespace emb;
+    if (K % 64 || N % 64 || M <= 0 || iters <= 0 || hip_device_count() == 0) return -1;
+    const int fdev = (fmt == FMT_F32 || fmt == FMT_F16) ? FMT_F16 : fmt;
+    const int Mp = (int)align_up((size_t)M, GEMM_BM);
+    const size_t nel = (size_t)N * K;
+    const size_t qbytes = fdev == FMT_F16 ? nel * 2 : (fdev == FMT_Q8_0 ? nel : nel / 2);
+    std::vector<uint8_t> hq(qbytes);
+    std::vector<uint16_t> hd(nel / 32), hx((size_t)Mp * K);
+    uint32_t st = 12345u;
+    auto rnd = [&]() { st = st * 1664525u + 1013904223u; return st; };
+    for (auto &b : hq) b = (uint8_t)(rnd() >> 24);
+    if (fdev == FMT_F16)
+        for (size_t i = 0; i < nel; ++i) ((uint16_t *)hq.data())[i] = f32_to_f16(((rnd() >> 8) / 16777216.0f - 0.5f) * 0.1f);
+    for (auto &v : hd) v = f32_to_f16(0.001f + (rnd() >> 8) / 16777216.0f * 0.01f);
+    for (auto &v : hx) v = f32_to_f16((rnd() >> 8) / 16777216.0f - 0.5f);
+    char *dq = nullptr, *dd = nullptr, *dx = nullptr, *db = nullptr, *dr = nullptr, *dout = nullptr;
+    HIP_RC(hipSetDevice(0));
+    HIP_RC(hipMalloc((void **)&dq, qbytes));
+    HIP_RC(hipMemcpy(dq, hq.data(), qbytes, hipMemcpyHostToDevice));
+    HIP_RC(hipMalloc((void **)&dd, hd.size() * 2));
+    HIP_RC(hipMemcpy(dd, hd.data(), hd.size() * 2, hipMemcpyHostToDevice));
+    HIP_RC(hipMalloc((void **)&dx, hx.size() * 2));
+    HIP_RC(hipMemcpy(dx, hx.data(), hx.size() * 2, hipMemcpyHostToDevice));
+    HIP_RC(hipMalloc((void **)&db, (size_t)N * 4));
+    HIP_RC(hipMemset(db, 0, (size_t)N * 4));
+    HIP_RC(hipMalloc((void **)&dr, (size_t)Mp * N * 4));
+    HIP_RC(hipMemset(dr, 0, (size_t)Mp * N * 4));
+    HIP_RC(hipMalloc((void **)&dout, (size_t)Mp * N * 4));
+    DevWeight W;
+    W.fmt = fdev; W.N = N; W.K = K;
+    W.qs = dq; W.d = (const uint16_t *)dd; W.m = (const uint16_t *)dd;
+    auto launch = [&]() {
+        if (ablate >= 0 && fdev == FMT_F16)
+            launch_gemm_ablation(W, (const uint16_t *)dx, Mp, (const float *)db, dout, nullptr, ablate,
+                                 tile_n ? tile_n : 256);
+        else {
+            g_force_bn = tile_n;
+            launch_gemm(W, (const uint16_t *)dx, Mp, (const float *)db, epi, (const float *)dr, dout, nullptr);
+            g_force_bn = 0;
+        }
+    };
+    for (int i = 0; i < 3; ++i) launch();
+    hipEvent_t a, b;
+    HIP_RC(hipEventCreate(&a));
+    HIP_RC(hipEventCreate(&b));
+    HIP_RC(hipEventRecord(a, nullptr));
+    for (int i = 0; i < iters; ++i) launch();
+    HIP_RC(hipEventRecord(b, nullptr));
+    HIP_RC(hipEventSynchronize(b));
+    float ms = 0.f;
+    HIP_RC(hipEventElapsedTime(&ms, a, b));
+    *avg_us = ms * 1000.0f / (float)iters;
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    for (char *p : {dq, dd, dx, db, dr, dout}) (void)hipFree(p);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -1,7 +1,7 @@
-// Fused dequant GEMM for gfx950:  Y[m][n] = epi( sum_k X[m][k] * W[n][k] )
+// f16-weight GEMM for gfx950:  Y[m][n] = epi( sum_k X[m][k] * W[n][k] )
 //   X  f16 [M][K] activations (tokens x features), M a multiple of 256
-//   W  [N][K] weights in the K-step-major repacked layout of kernels.h
-//      (f16, or q4_0 / q4_1 / q8_0 blocks dequantized on chip)
+//   W  f16 [N][K] weights (f16 files; f32 files converted at load) in the
+//      K-step-major layout of kernels.h.  Quantized weights: gemm_q.hip.
 //
 // Workgroup = 8 waves (4 along tokens x 2 along features), tile 256 tokens x BN
 // features x 64 k per step, BN = 256 for the wide projections (QKV, FFN-up)
@@ -105,126 +105,10 @@ struct WPath<FMT_F16, BN> {   // f16 (f32 files are converted at load)
     __device__ void expand(char *, const char *, int, int) const {}
 };
 
-// q4_0 / q4_1.  BN = 256: one 32-weight block per lane.  BN = 128: lanes 2i and
-// 2i+1 load the same block and expand one half each.
-template <int FMT, int BN>
-struct WPathQ4 {
-    static constexpr int LPB = BN == 256 ? 1 : 2;   // lanes per block
-    const uint8_t *pq;
-    const uint32_t *pd, *pm;
-    size_t step;
-    __device__ static int block(int wave, int lane) { return (64 / LPB) * wave + lane / LPB; }
-    __device__ void init(const DevWeight &W, int n0, int wave, int lane)
-    {
-        const int j = block(wave, lane);   // tile block: row j>>1, k-half j&1
-        const int n = min(n0 + (j >> 1), W.N - 1);
-        step = (size_t)W.N;
-        pq = (const uint8_t *)W.qs + ((size_t)n * 2 + (j & 1)) * 16;
-        pd = (const uint32_t *)W.d + n;
-        pm = FMT == FMT_Q4_1 ? (const uint32_t *)W.m + n : nullptr;
-    }
-    __device__ void issue(int ks, char *, char *raw, int wave) const
-    {
-        glds<16>(pq + ks * step * 32, raw + Cfg<BN>::OFF_RQ + 1024 * wave);
-        glds<4>(pd + ks * step, raw + Cfg<BN>::OFF_RS + 256 * wave);
-        if (FMT == FMT_Q4_1) glds<4>(pm + ks * step, raw + Cfg<BN>::OFF_RM + 256 * wave);
-    }
-    __device__ void expand(char *wst, const char *raw, int wave, int lane) const
-    {
-        const int j = block(wave, lane), r = j >> 1, blk = j & 1;
-        const int h = LPB == 2 ? (lane & 1) : 0;
-        const char *src = raw + Cfg<BN>::OFF_RQ + 1024 * wave + 16 * lane;
-        const uint32_t sd = *(const uint32_t *)(raw + Cfg<BN>::OFF_RS + 256 * wave + 4 * lane);
-        const h16 d = as_h((uint16_t)(blk ? sd >> 16 : sd & 0xffffu));
-        h16 m = (h16)0.0f;
-        if (FMT == FMT_Q4_1) {
-            const uint32_t sm = *(const uint32_t *)(raw + Cfg<BN>::OFF_RM + 256 * wave + 4 * lane);
-            m = as_h((uint16_t)(blk ? sm >> 16 : sm & 0xffffu));
-        }
-        const h16x2 d2 = {d, d}, m2 = {m, m};
-        const h16 o = FMT == FMT_Q4_1 ? (h16)-1024.0f : (h16)-1032.0f;
-        const h16x2 off = {o, o};
-        constexpr int NW = 4 / LPB;   // words this lane expands
-        uint32_t w[4];
-        if (LPB == 1) {
-            const uint4 q = *(const uint4 *)src;
-            w[0] = q.x; w[1] = q.y; w[2] = q.z; w[3] = q.w;
-        } else {
-            const uint2 q = *(const uint2 *)(src + 8 * h);
-            w[0] = q.x; w[1] = q.y;
-        }
-#pragma unroll
-        for (int t = 0; t < NW; ++t) {
-            h16x8 v;
-#pragma unroll
-            for (int p = 0; p < 4; ++p) {   // word: 8 k, element e at bit 4(e/2) + 16(e%2)
-                h16x2 hh = as_h2(((w[t] >> (4 * p)) & 0x000F000Fu) | 0x64006400u) + off;
-                hh = FMT == FMT_Q4_1 ? hh * d2 + m2 : hh * d2;
-                v[2 * p] = hh[0];
-                v[2 * p + 1] = hh[1];
-            }
-            *(h16x8 *)(wst + swz(r, 4 * blk + NW * h + t)) = v;
-        }
-    }
-};
-template <int BN> struct WPath<FMT_Q4_0, BN> : WPathQ4<FMT_Q4_0, BN> {};
-template <int BN> struct WPath<FMT_Q4_1, BN> : WPathQ4<FMT_Q4_1, BN> {};
+// Ablation switches (diagnostic builds only; production instantiates ABL = 0).
+enum : int { ABL_NO_LOADS = 1, ABL_NO_EXPAND = 2, ABL_NO_MFMA = 4, ABL_NO_EPILOGUE = 8 };
 
-// q8_0: 32 B per block.  BN = 256: one block per lane (two 16-B LDS-DMA);
-// BN = 128: half a block per lane.
-template <int BN>
-struct WPath<FMT_Q8_0, BN> {
-    static constexpr int LPB = BN == 256 ? 1 : 2;
-    const uint8_t *pq;
-    const uint32_t *pd;
-    size_t step;
-    __device__ static int block(int wave, int lane) { return (64 / LPB) * wave + lane / LPB; }
-    __device__ void init(const DevWeight &W, int n0, int wave, int lane)
-    {
-        const int j = block(wave, lane);
-        const int n = min(n0 + (j >> 1), W.N - 1);
-        step = (size_t)W.N;
-        pq = (const uint8_t *)W.qs + ((size_t)n * 2 + (j & 1)) * 32 + (LPB == 2 ? 16 * (lane & 1) : 0);
-        pd = (const uint32_t *)W.d + n;
-    }
-    __device__ void issue(int ks, char *, char *raw, int wave) const
-    {
-        char *dst = raw + Cfg<BN>::OFF_RQ + (LPB == 1 ? 2048 : 1024) * wave;
-        glds<16>(pq + ks * step * 64, dst);
-        if (LPB == 1) glds<16>(pq + ks * step * 64 + 16, dst + 1024);
-        glds<4>(pd + ks * step, raw + Cfg<BN>::OFF_RS + 256 * wave);
-    }
-    __device__ void expand(char *wst, const char *raw, int wave, int lane) const
-    {
-        const int j = block(wave, lane), r = j >> 1, blk = j & 1;
-        const int h = LPB == 2 ? (lane & 1) : 0;
-        const char *src = raw + Cfg<BN>::OFF_RQ + (LPB == 1 ? 2048 : 1024) * wave + 16 * lane;
-        const uint32_t sd = *(const uint32_t *)(raw + Cfg<BN>::OFF_RS + 256 * wave + 4 * lane);
-        const h16 d = as_h((uint16_t)(blk ? sd >> 16 : sd & 0xffffu));
-        const h16x2 d2 = {d, d};
-        const h16x2 off = {(h16)-1152.0f, (h16)-1152.0f};   // bytes hold q ^ 0x80, order e0 e2 e1 e3
-#pragma unroll
-        for (int half = 0; half < 2 / LPB; ++half) {
-            const uint4 q = *(const uint4 *)(src + 1024 * half);
-            const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-            h16x8 v[2];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const h16x2 a = (as_h2((w[t] & 0x00FF00FFu) | 0x64006400u) + off) * d2;
-                const h16x2 b = (as_h2(((w[t] >> 8) & 0x00FF00FFu) | 0x64006400u) + off) * d2;
-                v[t >> 1][4 * (t & 1) + 0] = a[0];
-                v[t >> 1][4 * (t & 1) + 1] = a[1];
-                v[t >> 1][4 * (t & 1) + 2] = b[0];
-                v[t >> 1][4 * (t & 1) + 3] = b[1];
-            }
-            const int c = 4 * blk + 2 * (h + half);
-            *(h16x8 *)(wst + swz(r, c)) = v[0];
-            *(h16x8 *)(wst + swz(r, c + 1)) = v[1];
-        }
-    }
-};
-
-template <int FMT, int EPI, int BN>
+template <int FMT, int EPI, int BN, int ABL = 0>
 __global__ __launch_bounds__(512, 1) void gemm_kernel(DevWeight W, const h16 *__restrict__ X,
                                                       const float *__restrict__ bias, const float *__restrict__ res,
                                                       void *__restrict__ out, int nN, int nTiles)
@@ -277,7 +161,7 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(DevWeight W, const h16 *__
         const bool more = ks + 1 < KS;
         const int xs_nxt = xs_cur + 1 == C::XS ? 0 : xs_cur + 1;
         const int xs_nn = xs_nxt + 1 == C::XS ? 0 : xs_nxt + 1;
-        if (more) {
+        if (more && !(ABL & ABL_NO_LOADS)) {
             wp.issue(ks + 1, smem + C::OFF_W + ((ks + 1) & 1) * C::W_BYTES, smem, wave);
             if (C::XS == 2) xsrc.issue(ks + 1, smem + C::OFF_X + xs_nxt * C::X_BYTES, wave);
         }
@@ -301,13 +185,18 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(DevWeight W, const h16 *__
                 nb0 = *(const h16x8 *)(xs + rb0 + cx);
                 nb1 = *(const h16x8 *)(xs + rb1 + cx);
             }
-            __builtin_amdgcn_s_setprio(1);
+            if constexpr (!(ABL & ABL_NO_MFMA)) {
+                __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-            for (int i = 0; i < NI; ++i) {
-                acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b0, acc[i][0], 0, 0, 0);
-                acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b1, acc[i][1], 0, 0, 0);
+                for (int i = 0; i < NI; ++i) {
+                    acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b0, acc[i][0], 0, 0, 0);
+                    acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b1, acc[i][1], 0, 0, 0);
+                }
+                __builtin_amdgcn_s_setprio(0);
+            } else {
+#pragma unroll
+                for (int i = 0; i < NI; ++i) asm volatile("" ::"v"(a[i]), "v"(b0), "v"(b1));
             }
-            __builtin_amdgcn_s_setprio(0);
             if (kk < 3) {
 #pragma unroll
                 for (int i = 0; i < NI; ++i) a[i] = na[i];
@@ -317,14 +206,24 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(DevWeight W, const h16 *__
         }
         if (more) {
             wait_vmcnt<0>();
-            wp.expand(smem + C::OFF_W + ((ks + 1) & 1) * C::W_BYTES, smem, wave, lane);
-            if (C::XS == 3 && ks + 2 < KS) xsrc.issue(ks + 2, smem + C::OFF_X + xs_nn * C::X_BYTES, wave);
+            if constexpr (!(ABL & ABL_NO_EXPAND)) wp.expand(smem + C::OFF_W + ((ks + 1) & 1) * C::W_BYTES, smem, wave, lane);
+            if (C::XS == 3 && ks + 2 < KS && !(ABL & ABL_NO_LOADS))
+                xsrc.issue(ks + 2, smem + C::OFF_X + xs_nn * C::X_BYTES, wave);
             lds_barrier();
         }
         xs_cur = xs_nxt;
     }
 
     // ---- epilogue ----
+    if constexpr ((ABL & ABL_NO_EPILOGUE) != 0) {   // keep the accumulators alive, store one word per lane
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s += acc[i][0][r] + acc[i][1][r];
+        ((float *)out)[(size_t)blockIdx.x * 512 + tid] = s;
+        return;
+    }
     lds_barrier();   // every wave is done with the operand stages
     if constexpr (EPI == EPI_BIAS_RES_F32) {
         // f32 staging: 256 rows x (BN*4 + 16) B, then res + (bias + acc) per 16-B chunk
@@ -422,15 +321,44 @@ void dispatch(const DevWeight &W, const uint16_t *X, int M, const float *bias, i
 
 }  // namespace
 
+// Diagnostic: f16-weight / EPI_BIAS_F16 GEMM with ablation switches, tile 128 or 256.
+template <int BN, int ABL>
+static void abl_one(const DevWeight &W, const h16 *x, int M, const float *bias, void *out, hipStream_t s)
+{
+    const int nN = (W.N + BN - 1) / BN, nTiles = (M / GM) * nN;
+    gemm_kernel<FMT_F16, EPI_BIAS_F16, BN, ABL><<<nTiles, 512, 0, s>>>(W, x, bias, nullptr, out, nN, nTiles);
+}
+
+template <int BN>
+static void abl_bn(const DevWeight &W, const h16 *x, int M, const float *bias, void *out, hipStream_t s, int abl)
+{
+    switch (abl) {
+    case 0: abl_one<BN, 0>(W, x, M, bias, out, s); break;
+    case 1: abl_one<BN, 1>(W, x, M, bias, out, s); break;
+    case 2: abl_one<BN, 2>(W, x, M, bias, out, s); break;
+    case 3: abl_one<BN, 3>(W, x, M, bias, out, s); break;
+    case 4: abl_one<BN, 4>(W, x, M, bias, out, s); break;
+    case 6: abl_one<BN, 6>(W, x, M, bias, out, s); break;
+    case 8: abl_one<BN, 8>(W, x, M, bias, out, s); break;
+    case 11: abl_one<BN, 11>(W, x, M, bias, out, s); break;
+    default: abl_one<BN, 15>(W, x, M, bias, out, s); break;
+    }
+}
+
+void launch_gemm_ablation(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, void *out,
+                          hipStream_t s, int32_t abl, int32_t bn)
+{
+    if (bn == 256) abl_bn<256>(W, (const h16 *)X, M, bias, out, s, abl);
+    else abl_bn<128>(W, (const h16 *)X, M, bias, out, s, abl);
+}
+
 void launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi, const float *res,
                  void *out, hipStream_t s)
 {
-    switch (W.fmt) {
-    case FMT_Q4_0: dispatch<FMT_Q4_0>(W, X, M, bias, epi, res, out, s); break;
-    case FMT_Q4_1: dispatch<FMT_Q4_1>(W, X, M, bias, epi, res, out, s); break;
-    case FMT_Q8_0: dispatch<FMT_Q8_0>(W, X, M, bias, epi, res, out, s); break;
-    default: dispatch<FMT_F16>(W, X, M, bias, epi, res, out, s); break;
-    }
+    if (W.fmt == FMT_Q4_0 || W.fmt == FMT_Q4_1 || W.fmt == FMT_Q8_0)
+        launch_gemm_q(W, X, M, bias, epi, res, out, s, g_force_bn);   // weights in registers (gemm_q.hip)
+    else
+        dispatch<FMT_F16>(W, X, M, bias, epi, res, out, s);
 }
 
 }  // namespace emb

@@ -5,12 +5,15 @@
 //            blocks): element (n, k) lives in step ks = k/64 at
 //            ((ks*N + n) * 64 + k%64) -- one K-step of a 128-row tile is one
 //            contiguous, fully coalesced run of bytes.
-//              f16 : 128 B per (ks, n)
-//              q4_0/q4_1: 32 B nibbles per (ks, n) = 2 blocks x 4 words; word w
-//                    of a block holds k = 8w..8w+7 with element e at bit
-//                    4*(e/2) + 16*(e%2) so one AND/OR yields an f16 pair;
-//                    d (and m) f16 [ks][n][2]
-//              q8_0: 64 B per (ks, n), bytes (q ^ 0x80) in order e0 e2 e1 e3 per
+//              f16 : 128 B per (ks, n), k ascending (LDS-staged GEMM)
+//              q4_0/q4_1: 32 B nibbles per (ks, n) in the MFMA A-fragment
+//                    ("register") order of gemm_q.hip: word 4h + kk holds
+//                    k = 16kk + 8h + i (i = 0..7), element i at bit
+//                    4*(i/2) + 16*(i%2) so one AND/OR yields an f16 pair; the
+//                    lane of half h loads its 4 words as one 16-B load.
+//                    d (and m) f16 [ks][n][2] (blocks k<32, k>=32)
+//              q8_0: 64 B per (ks, n): 8 bytes per (h, kk) at 32h + 8kk holding
+//                    k = 16kk + 8h + i as (q ^ 0x80), order e0 e2 e1 e3 per
 //                    4-group (pair extraction by mask); d f16 [ks][n][2]
 //   QKV      the three projections are one [3d][d] weight (one GEMM, N = 3d)
 //   tables   word/type/pos embeddings in the file's format; q blocks split
@@ -51,8 +54,17 @@ constexpr int ATT_QT = 128;           // queries per attention workgroup
 void launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi,
                  const float *res, void *out, hipStream_t s);
 
+// Quantized-weight GEMM (gemm_q.hip); force_bn: 0 = heuristic, 128 / 256.
+void launch_gemm_q(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi,
+                   const float *res, void *out, hipStream_t s, int32_t force_bn);
+
 // Tests only: force the GEMM tile width (128 / 256; 0 = heuristic).
 extern int g_force_bn;
+
+// Diagnostics only: q4_0 GEMM with parts switched off (1 no per-step loads,
+// 2 no dequant, 4 no MFMA, 8 no epilogue; combinations 3, 6, 11, 15).
+void launch_gemm_ablation(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, void *out,
+                          hipStream_t s, int32_t abl, int32_t bn);
 
 // x = LN(pos[i] + (type[0] + word[id])) for every valid token (bert.cpp:963-984).
 void launch_embed_ln(const DevTable &word, const DevTable &type, const DevTable &pos, const float *ln_w,

@@ -69,6 +69,15 @@ BERT_API int32_t bertx_test_gemm(int32_t fmt, int32_t N, int32_t K, const void *
                                  const float *bias, int32_t M, const uint16_t *x,
                                  int32_t epi, const float *res, void *out, int32_t tile_n);
 
+/*
+ * GEMM micro-benchmark on random operands (device 0): average device time of
+ * `iters` launches of the production GEMM for fmt / N / K / M / epi (tile_n 0 =
+ * production choice).  ablate >= 0 selects a diagnostic q4_0 build with parts
+ * switched off (1 per-step loads, 2 dequant, 4 MFMA, 8 epilogue; 3, 6, 11, 15).
+ */
+BERT_API int32_t bertx_bench_gemm(int32_t fmt, int32_t N, int32_t K, int32_t M, int32_t epi, int32_t tile_n,
+                                  int32_t ablate, int32_t iters, float *avg_us);
+
 BERT_API const char *bertx_version(void);
 
 #ifdef __cplusplus
