@@ -58,8 +58,29 @@ def algorithmic_bytes(hp, ftype, B, L):
     d, f, nl = hp["n_embd"], hp["n_intermediate"], hp["n_layer"]
     w = nl * (4 * d * d + 2 * d * f) * bpw
     small = nl * (9 * d + f) * 4 + 4 * d * 4
-    emb_rows = B * L * d * bpw * 2 + 2 * d * bpw
+    emb_rows = B * L * d * bpw + L * d * bpw + 2 * d * bpw   # word row per token; position / type tables once
     return w + small + emb_rows + 4 * B * L + 4 * B * d
+
+
+def timed_steps(step, steps, sync, dist=None, reduce_device="cpu"):
+    """The contract's timed region: barrier + sync, `steps` steps, sync + barrier;
+    returns the MAX over ranks of the elapsed seconds (every rank gets it)."""
+    if dist is not None:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=reduce_device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    return elapsed
 
 
 def main():
@@ -118,21 +139,8 @@ def main():
 
     lib.bertx_set_profiling(ctx, 0 if a.no_profile else 1)
     lib.bertx_reset_stats(ctx)
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    if dist is not None:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if dist is not None:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    red_dev = dev if (dist is not None and dist.get_backend() == "nccl") else "cpu"
+    elapsed = timed_steps(step, a.steps, lambda: torch.cuda.synchronize(dev), dist, red_dev)
     lib.bertx_set_profiling(ctx, 0)
     stats = model.kernel_stats()
 

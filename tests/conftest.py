@@ -1,4 +1,6 @@
+import json
 import os
+import subprocess
 import sys
 
 import pytest
@@ -14,14 +16,39 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); calls the HIP path through the C ABI")
 
 
+def _ensure(artifact, make_dir):
+    """Build an in-tree artifact if it is missing (the driver's build() normally made it)."""
+    if not os.path.exists(artifact):
+        subprocess.run(["make", "-C", make_dir, "-j8"], check=True, stdout=subprocess.DEVNULL)
+    assert os.path.exists(artifact), artifact
+
+
+LIB_SO = os.path.join(ROOT, "build", "libbert.so")
+ORACLE_SO = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
+
+
 @pytest.fixture(scope="session")
 def lib():
+    _ensure(LIB_SO, os.path.join(ROOT, "embeddings.cpp_amd"))
     import bertpy
     return bertpy.load_lib()
 
 
 @pytest.fixture(scope="session")
-def quant_models(tmp_path_factory):
+def oracle():
+    _ensure(ORACLE_SO, os.path.join(ROOT, "oracle"))
+    import oracle_lib
+    return oracle_lib
+
+
+@pytest.fixture(scope="session")
+def tok_golden():
+    with open(os.path.join(GOLDEN, "tokenizer_cases.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def quant_models(tmp_path_factory, oracle):
     """tiny32/tiny64 in every format: f32/f16 from the reference converter (committed),
     q4_0/q4_1/q8_0 quantized from the f16 file by the ORACLE quantizer (run_conversions.sh order)."""
     import oracle_lib

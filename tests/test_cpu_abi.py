@@ -1,0 +1,181 @@
+"""CPU tests of the product library's boundary (no GPU compute):
+
+  * libbert.so loads and exports every function include/*.h declares;
+  * without a HIP device bert_load_from_file fails loudly (no CPU compute path);
+  * the host side behind the ABI -- model-file loader, tokenizer, quantizer --
+    in a tokenizer-only context (BERT_HOST_ONLY=1), checked bit-exact against
+    the reference's golden token ids and the oracle's quantizer bytes.
+"""
+import ctypes
+import glob
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT
+from test_cpu_oracle import expected_id_to_token
+
+HAS_GPU_NODE = os.path.exists("/dev/kfd")
+
+
+def declared_functions():
+    names = set()
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        src = re.sub(r"//[^\n]*", "", src)
+        for m in re.finditer(r"\b((?:bert|bertx|ggml)_[a-z0-9_]+)\s*\(", src):
+            names.add(m.group(1))
+    return names
+
+
+def test_exports_every_declared_symbol(lib):
+    names = declared_functions()
+    assert {"bert_load_from_file", "bert_encode_batch", "bert_forward_batch", "bert_tokenize",
+            "bertx_forward_device", "ggml_time_us"} <= names
+    missing = [n for n in sorted(names) if not hasattr(lib, n)]
+    assert not missing, missing
+    nm = subprocess.run(["nm", "-D", "--defined-only", os.path.join(ROOT, "build", "libbert.so")],
+                        capture_output=True, text=True, check=True).stdout
+    exported = {ln.split()[-1] for ln in nm.splitlines() if " T " in ln}
+    assert names <= exported, names - exported
+    # nothing but the ABI leaks out (hidden visibility for everything else)
+    assert {n for n in exported if not n.startswith(("bert", "ggml_"))} <= {"_init", "_fini"}
+
+
+def test_version_and_time(lib):
+    v = lib.bertx_version().decode()
+    assert "gfx950" in v
+    t0 = lib.ggml_time_us()
+    t1 = lib.ggml_time_us()
+    assert t1 >= t0 >= 0
+
+
+@pytest.mark.skipif(HAS_GPU_NODE, reason="checks the no-device failure path")
+def test_load_without_device_fails_loudly(lib, monkeypatch):
+    monkeypatch.delenv("BERT_HOST_ONLY", raising=False)
+    ctx = lib.bert_load_from_file(os.path.join(GOLDEN, "tiny32", "ggml-model-f32.bin").encode())
+    assert not ctx
+
+
+@pytest.fixture
+def host_model(lib, monkeypatch):
+    import bertpy
+    monkeypatch.setenv("BERT_HOST_ONLY", "1")
+    m = bertpy.BertModel(os.path.join(GOLDEN, "tiny32", "ggml-model-f32.bin"), lib=lib)
+    yield m
+    del m
+
+
+def test_host_context_metadata(host_model, tok_golden):
+    assert host_model.n_embd == 64 and host_model.n_max_tokens == 128
+    n_vocab, n_max, d, f, h, nl, ftype = host_model.hparams()
+    assert (n_vocab, n_max, d, f, h, nl, ftype) == (len(tok_golden["vocab"]), 128, 64, 128, 2, 2, 0)
+    assert host_model.lib.bertx_num_devices(host_model.ctx) == 0
+    exp = expected_id_to_token(tok_golden["vocab"])
+    assert [host_model.id_to_token(i).decode() for i in range(len(exp))] == exp
+
+
+def test_host_tokenizer_matches_reference_goldens(host_model, tok_golden):
+    """Token ids bit-exact.  The reference's n_max_tokens is checked only between
+    words (bert.cpp:386), so its count can exceed it (it then writes past the
+    caller's buffer); the product reports the same count but never writes past
+    n_max_tokens, so the written prefix is compared."""
+    bad, over = [], 0
+    for c in tok_golden["cases"]:
+        ids, n = host_model.tokenize(bytes.fromhex(c["text_hex"]), c["n_max_tokens"])
+        g = c["ids"]
+        over += n > c["n_max_tokens"]
+        if n != len(g) or ids != g[: c["n_max_tokens"]]:
+            bad.append((bytes.fromhex(c["text_hex"])[:30], n, len(g), ids[:8], g[:8]))
+    assert not bad, bad[:5]
+    assert over > 0     # the goldens do exercise the overflow quirk
+
+
+def test_host_tokenizer_matches_oracle_on_random_text(host_model, oracle):
+    """Random UTF-8 mixes (ASCII, punctuation, accents, CJK, invalid bytes)."""
+    orc = oracle.Oracle(os.path.join(GOLDEN, "tiny32", "ggml-model-f32.bin"))
+    rng = np.random.default_rng(3)
+    alphabet = list("abcdefghijklmnopqrstuvwxyz     ,.!?'-0123456789") + ["é", "Ü", "ß", "中", "日", "本", "\t",
+                                                                          "\n", "ﬁ", "Æ", "##"]
+    for i in range(300):
+        n = int(rng.integers(0, 80))
+        s = "".join(alphabet[j] for j in rng.integers(0, len(alphabet), n)).encode()
+        if i % 10 == 0:
+            s += bytes([0xff, 0xc3])           # invalid / truncated UTF-8 tail
+        for n_max in (128, 7):
+            ids, n = host_model.tokenize(s, n_max)
+            ref = orc.tokenize(s, n_max)
+            assert n == len(ref) and ids == ref[:n_max], (s, n_max)
+
+
+def test_host_forward_refused(host_model):
+    """A tokenizer-only context has no compute path: forward leaves outputs alone."""
+    out = host_model.forward_batch([[101, 150, 102]], fill=7.0)
+    assert np.all(out == 7.0)
+
+
+@pytest.mark.parametrize("bad", ["missing", "empty", "magic", "truncated"])
+def test_bad_model_files(lib, tmp_path, monkeypatch, bad):
+    monkeypatch.setenv("BERT_HOST_ONLY", "1")
+    src = open(os.path.join(GOLDEN, "tiny32", "ggml-model-f16.bin"), "rb").read()
+    p = tmp_path / "m.bin"
+    if bad == "empty":
+        p.write_bytes(b"")
+    elif bad == "magic":
+        p.write_bytes(b"\0\0\0\0" + src[4:])
+    elif bad == "truncated":
+        p.write_bytes(src[: len(src) // 2])
+    assert not lib.bert_load_from_file(str(p).encode())
+
+
+@pytest.mark.parametrize("itype", [2, 3, 8])
+@pytest.mark.parametrize("tiny,src", [("tiny32", "f32"), ("tiny64", "f16")])
+def test_quantizer_bytes_match_oracle(lib, oracle, tmp_path, tiny, src, itype):
+    """bertx_quantize_file (and the quantize CLI) == the oracle quantizer, byte for byte."""
+    fin = os.path.join(GOLDEN, tiny, f"ggml-model-{src}.bin")
+    a, b, c = str(tmp_path / "prod.bin"), str(tmp_path / "orc.bin"), str(tmp_path / "cli.bin")
+    assert lib.bertx_quantize_file(fin.encode(), a.encode(), itype) == 0
+    assert oracle.quantize_file(fin, b, itype) == 0
+    assert open(a, "rb").read() == open(b, "rb").read()
+    cli = os.path.join(ROOT, "build", "bin", "quantize")
+    if os.path.exists(cli):
+        r = subprocess.run([cli, fin, c, str(itype)], capture_output=True)
+        assert r.returncode == 0
+        assert open(c, "rb").read() == open(b, "rb").read()
+
+
+def test_quantizer_rejects_bad_type(lib, tmp_path):
+    fin = os.path.join(GOLDEN, "tiny32", "ggml-model-f32.bin")
+    assert lib.bertx_quantize_file(fin.encode(), str(tmp_path / "x.bin").encode(), 5) != 0
+    assert lib.bertx_quantize_file(b"/nonexistent/model.bin", str(tmp_path / "y.bin").encode(), 2) != 0
+    cli = os.path.join(ROOT, "build", "bin", "quantize")
+    if os.path.exists(cli):
+        assert subprocess.run([cli], capture_output=True).returncode != 0
+
+
+def test_quantized_file_loads_in_host_context(lib, tmp_path, monkeypatch):
+    import bertpy
+    monkeypatch.setenv("BERT_HOST_ONLY", "1")
+    q = str(tmp_path / "q.bin")
+    assert lib.bertx_quantize_file(os.path.join(GOLDEN, "tiny64", "ggml-model-f16.bin").encode(), q.encode(), 2) == 0
+    m = bertpy.BertModel(q, lib=lib)
+    assert m.hparams()[6] == 2 and m.n_embd == 64
+
+
+def test_synthetic_model_writer_roundtrip(lib, oracle, tmp_path, monkeypatch):
+    """bertpy's reference-format writer (bench / tests) produces files both the
+    product loader and the oracle accept with the same header."""
+    import bertpy
+    monkeypatch.setenv("BERT_HOST_ONLY", "1")
+    hp = dict(n_vocab=300, n_max_tokens=64, n_embd=64, n_intermediate=128, n_head=2, n_layer=1)
+    p = str(tmp_path / "syn.bin")
+    bertpy.write_model(p, hp, bertpy.synthetic_vocab(300), bertpy.synthetic_tensors(hp), 1)
+    m = bertpy.BertModel(p, lib=lib)
+    o = oracle.Oracle(p)
+    assert m.hparams()[:6] == [o.n_vocab, o.n_max_tokens, o.n_embd, o.n_intermediate, o.n_head, o.n_layer]
+    assert m.hparams()[:6] == [300, 64, 64, 128, 2, 1]
+    assert ctypes.sizeof(ctypes.c_int32) == 4

@@ -1,0 +1,88 @@
+"""Multi-process (gloo, world_size 2, CPU) tests of bench.py's distributed
+contract: the path is embarrassingly parallel (one replica per GPU, no data-path
+collective); the only cross-rank traffic is the barrier pair and the MAX
+all-reduce of the timed region."""
+import os
+import socket
+import sys
+import time
+
+import numpy as np
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+sys.path.insert(0, ROOT)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    calls = []
+    step_s = 0.02 * (rank + 1)                       # rank 1 is the straggler
+
+    def step():
+        calls.append(1)
+        time.sleep(step_s)
+
+    el = bench.timed_steps(step, 5, lambda: None, dist, "cpu")
+    r, w, lr = bench.dist_env()
+    q.put((rank, el, len(calls), (r, w, lr)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_timed_steps_max_over_ranks_gloo():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort()
+    els = [r[1] for r in res]
+    assert els[0] == els[1]                       # every rank reports the same (max) time
+    assert els[0] >= 5 * 0.04 * 0.95              # at least the straggler's work
+    assert all(r[2] == 5 for r in res)            # exactly K timed steps per rank
+    assert [r[3] for r in res] == [(0, 2, 0), (1, 2, 1)]
+
+
+def test_timed_steps_single_process():
+    import bench
+    n = []
+    el = bench.timed_steps(lambda: n.append(0), 7, lambda: None, None)
+    assert len(n) == 7 and el >= 0
+
+
+def test_rank_shards_are_distinct():
+    """Each rank encodes its own shard (weak scaling): seeds differ per rank."""
+    import bertpy
+    a = bertpy.synthetic_ids(4, 16, 30522, seed=7 + 0)
+    b = bertpy.synthetic_ids(4, 16, 30522, seed=7 + 1)
+    assert not all(np.array_equal(x, y) for x, y in zip(a, b))
+    assert all(x[0] == 101 and x[-1] == 102 for x in a + b)
+
+
+def test_algorithmic_bytes_bge_base_q4_0():
+    """Compulsory HBM bytes per batch (DESIGN.md "Roofline"): weights at 4.5 bits
+    plus one gathered word-embedding row per token; activations not counted."""
+    import bench
+    import bertpy
+    b = bench.algorithmic_bytes(bertpy.ARCHS["bge-base-en-v1.5"], "q4_0", 64, 512)
+    w = 12 * (4 * 768 * 768 + 2 * 768 * 3072) * 0.5625
+    rows = 64 * 512 * 768 * 0.5625
+    assert w + rows < b < (w + rows) * 1.05
