@@ -50,12 +50,16 @@ __global__ __launch_bounds__(256) void attention_kernel(const h16 *__restrict__ 
         // K tile row-major (coalesced: chunk index fastest)
         for (int c = tid; c < KT * DH / 8; c += 256) {
             const int r = c / (DH / 8), ch = c % (DH / 8);
-            *(uint4 *)(Ks + r * KSTR + ch * 8) = *(const uint4 *)(qkv + (size_t)(start + k0 + r) * ld + d + h * DH + ch * 8);
+            uint4 kv = {0u, 0u, 0u, 0u};
+            if (k0 + r < len) kv = *(const uint4 *)(qkv + (size_t)(start + k0 + r) * ld + d + h * DH + ch * 8);
+            *(uint4 *)(Ks + r * KSTR + ch * 8) = kv;
         }
         // V tile transposed into Vt[d][key] (key fastest across lanes: conflict-free 2-byte writes)
         for (int c = tid; c < KT * DH / 8; c += 256) {
             const int r = c % KT, ch = c / KT;
-            const h16x8 vv = *(const h16x8 *)(qkv + (size_t)(start + k0 + r) * ld + 2 * d + h * DH + ch * 8);
+            // keys past the sentence: zeros (their P is exactly 0; 0 * garbage could be NaN)
+            h16x8 vv = {};
+            if (k0 + r < len) vv = *(const h16x8 *)(qkv + (size_t)(start + k0 + r) * ld + 2 * d + h * DH + ch * 8);
 #pragma unroll
             for (int e = 0; e < 8; ++e) Vt[(ch * 8 + e) * VSTR + r] = vv[e];
         }

@@ -49,7 +49,8 @@ std::vector<int> parse_device_list(int n_visible)
         const std::string tok = s.substr(p, q - p);
         if (!tok.empty()) {
             const int v = std::atoi(tok.c_str());
-            if (v >= 0 && v < n_visible && std::find(out.begin(), out.end(), v) == out.end()) out.push_back(v);
+            // a repeated ordinal is a second replica (own stream + workspace) on that device
+            if (v >= 0 && v < n_visible) out.push_back(v);
         }
         p = q + 1;
     }

@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 namespace emb {
@@ -289,7 +290,10 @@ bool Device::reserve(int64_t tokens, int64_t seqs)
     if (h_out_) { (void)hipHostFree(h_out_); h_out_ = nullptr; }
     cap_tokens_ = cap_seqs_ = 0;
     HIP_OK(hipMalloc((void **)&ws_, off));
-    HIP_OK(hipMemset(ws_, 0, off));
+    // on the replica's own (non-blocking) stream: a null-stream memset would not
+    // be ordered before the forward that follows on stream_
+    HIP_OK(hipMemsetAsync(ws_, 0, off, stream_));
+    HIP_OK(hipStreamSynchronize(stream_));
     x32_ = (float *)(ws_ + o_x32); y32_ = (float *)(ws_ + o_y32); xh_ = (uint16_t *)(ws_ + o_xh);
     qkv_ = (uint16_t *)(ws_ + o_qkv); att_ = (uint16_t *)(ws_ + o_att); ffn_ = (uint16_t *)(ws_ + o_ffn);
     d_ids_ = (int32_t *)(ws_ + o_ids); d_cu_ = (int32_t *)(ws_ + o_cu); d_out_ = (float *)(ws_ + o_out);
@@ -360,10 +364,29 @@ int Device::forward(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, int m
     const int M = (int)align_up((size_t)T, GEMM_BM);
     const double t = (double)T;
     hipEvent_t ev;
+    // BERT_CHECK_FINITE=1: after every kernel, count non-finite outputs over the
+    // valid rows and report the first kernel that produced any (diagnostics).
+    static const bool check = [] { const char *e = std::getenv("BERT_CHECK_FINITE"); return e && *e == '1'; }();
+    unsigned *cnt = nullptr;
+    bool bad = false;
+    if (check) (void)hipMalloc((void **)&cnt, sizeof(unsigned));
+    auto chk = [&](const char *what, int layer, const void *p, size_t n, int f16) {
+        if (!check || bad) return;
+        (void)hipMemsetAsync(cnt, 0, sizeof(unsigned), s);
+        launch_count_nonfinite(p, n, f16, cnt, s);
+        unsigned h = 0;
+        (void)hipMemcpyAsync(&h, cnt, sizeof(unsigned), hipMemcpyDeviceToHost, s);
+        (void)hipStreamSynchronize(s);
+        if (h) {
+            bad = true;
+            std::fprintf(stderr, "libbert: BERT_CHECK_FINITE: %u non-finite values after %s (layer %d)\n", h, what, layer);
+        }
+    };
 
     begin(K_EMBED_LN, s, ev);
     launch_embed_ln(word_, type_, pos_, ln_e_w_, ln_e_b_, d_ids, d_cu, n_seqs, max_len, d, x32_, xh_, s);
     end(K_EMBED_LN, s, ev, t * (4.0 + 3.0 * d * 2.0 + 6.0 * d));
+    chk("embed_ln", -1, x32_, (size_t)T * d, 0);
 
     const double att_flop = 4.0 * (double)d * t * (double)max_len;   // exact when all lengths are equal
     for (int l = 0; l < hp_.n_layer; ++l) {
@@ -371,34 +394,43 @@ int Device::forward(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, int m
         begin(K_GEMM_QKV, s, ev);
         launch_gemm(L.qkv, xh_, M, L.b_qkv, EPI_BIAS_F16, nullptr, qkv_, s);
         end(K_GEMM_QKV, s, ev, 2.0 * t * 3.0 * d * d);
+        chk("gemm_qkv", l, qkv_, (size_t)T * 3 * d, 1);
 
         begin(K_ATTENTION, s, ev);
         launch_attention(qkv_, d_cu, n_seqs, max_len, hp_.n_head, d, att_, s);
         end(K_ATTENTION, s, ev, att_flop);
+        chk("attention", l, att_, (size_t)T * d, 1);
 
         begin(K_GEMM_O, s, ev);
         launch_gemm(L.o, att_, M, L.b_o, EPI_BIAS_RES_F32, x32_, y32_, s);
         end(K_GEMM_O, s, ev, 2.0 * t * d * d);
+        chk("gemm_o", l, y32_, (size_t)T * d, 0);
 
         begin(K_LAYERNORM, s, ev);
         launch_layernorm(y32_, T, d, L.ln1_w, L.ln1_b, x32_, xh_, s);
         end(K_LAYERNORM, s, ev, t * d * 10.0);
+        chk("layernorm1", l, x32_, (size_t)T * d, 0);
 
         begin(K_GEMM_FFN_UP, s, ev);
         launch_gemm(L.up, xh_, M, L.b_up, EPI_BIAS_GELU_F16, nullptr, ffn_, s);
         end(K_GEMM_FFN_UP, s, ev, 2.0 * t * d * f);
+        chk("gemm_up", l, ffn_, (size_t)T * f, 1);
 
         begin(K_GEMM_FFN_DOWN, s, ev);
         launch_gemm(L.down, ffn_, M, L.b_down, EPI_BIAS_RES_F32, x32_, y32_, s);
         end(K_GEMM_FFN_DOWN, s, ev, 2.0 * t * d * f);
+        chk("gemm_down", l, y32_, (size_t)T * d, 0);
 
         begin(K_LAYERNORM, s, ev);
         launch_layernorm(y32_, T, d, L.ln2_w, L.ln2_b, x32_, xh_, s);
         end(K_LAYERNORM, s, ev, t * d * 10.0);
+        chk("layernorm2", l, x32_, (size_t)T * d, 0);
     }
     begin(K_POOL_L2, s, ev);
     launch_pool_l2(x32_, d_cu, n_seqs, max_len, d, pool_part_, d_out, s);
     end(K_POOL_L2, s, ev, t * d * 4.0 + (double)n_seqs * d * 4.0);
+    chk("pool_l2", -1, d_out, (size_t)n_seqs * d, 0);
+    if (cnt) (void)hipFree(cnt);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         std::fprintf(stderr, "libbert: kernel launch failed: %s\n", hipGetErrorString(e));

@@ -15,9 +15,13 @@
 // and 4 B fragments per k-slice.  MFMA v_mfma_f32_32x32x16_f16, A = W rows,
 // B = X rows (the accumulator lane is a token).
 //
-// Loads issued per K-step (asm, so the compiler's waitcnt pass cannot drain
-// the LDS-DMA ring for them): W(ks+1) to registers, then X(ks+2) by LDS-DMA;
-// at the end of the step `s_waitcnt vmcnt(4)` retires everything but X(ks+2).
+// Per K-step: W(ks+1) to the other register set (ordinary loads), then
+// X(ks+2) by LDS-DMA, then an explicit `s_waitcnt vmcnt(loads issued)` -- a
+// run-time no-op that tells the compiler the current set has landed, so its
+// waitcnt pass adds no vmcnt(0) (which would drain the ring) before the MFMAs.
+// The loop is branch-free (past the end the issues re-read step KS-1), so the
+// compiler sees a fixed count on every path.  At the end of the step
+// `s_waitcnt vmcnt(4)` retires everything but X(ks+2).
 #include "device_common.h"
 #include "host_common.h"
 #include "kernels.h"

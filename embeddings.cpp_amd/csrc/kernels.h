@@ -86,4 +86,7 @@ int32_t pool_chunks(int32_t max_len);
 void launch_pool_l2(const float *x32, const int32_t *cu, int32_t n_seqs, int32_t max_len, int32_t d, float *partial,
                     float *out, hipStream_t s);
 
+// Diagnostics: *cnt += number of non-finite values in p[0..n) (f32, or f16 if f16).
+void launch_count_nonfinite(const void *p, size_t n, int f16, unsigned *cnt, hipStream_t s);
+
 }  // namespace emb

@@ -172,7 +172,23 @@ __global__ __launch_bounds__(256) void pool_final_kernel(const float *__restrict
     for (int c = tid; c < d; c += 256) out[(size_t)b * d + c] = e[ne++] / nrm;
 }
 
+// diagnostics (BERT_CHECK_FINITE): count non-finite values of a buffer
+__global__ void count_nonfinite_kernel(const void *p, size_t n, int f16, unsigned *cnt)
+{
+    unsigned c = 0;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const float v = f16 ? (float)((const h16 *)p)[i] : ((const float *)p)[i];
+        c += !__builtin_isfinite(v);
+    }
+    if (c) atomicAdd(cnt, c);
+}
+
 }  // namespace
+
+void launch_count_nonfinite(const void *p, size_t n, int f16, unsigned *cnt, hipStream_t s)
+{
+    count_nonfinite_kernel<<<1024, 256, 0, s>>>(p, n, f16, cnt);
+}
 
 void launch_embed_ln(const DevTable &word, const DevTable &type, const DevTable &pos, const float *ln_w,
                      const float *ln_b, const int32_t *ids, const int32_t *cu, int32_t n_seqs, int32_t max_len,

@@ -118,3 +118,47 @@ def test_bge_base_q4_0_full_size(tmp_path):
     assert np.array_equal(two, full[:2])
     ref = oracle_lib.Oracle(path).forward_batch(ids[:2], n_threads=min(16, os.cpu_count() or 1))
     assert np.all(cosines(full[:2], ref) >= 1 - COS_TOL)
+
+
+def test_two_replicas_on_one_device_bitwise(quant_models, monkeypatch):
+    """In-process sharding (bert_abi.cpp run_forward): BERT_DEVICES=0,0 gives two
+    replicas with their own streams; outputs are bitwise those of one replica."""
+    path = quant_models[("tiny64", "q4_0")]
+    ids = ragged_ids(690, [5, 300, 512, 40, 2, 129, 77, 250, 3])
+    one = bertpy.BertModel(path).forward_batch(ids)
+    monkeypatch.setenv("BERT_DEVICES", "0,0")
+    m2 = bertpy.BertModel(path)
+    assert m2.lib.bertx_num_devices(m2.ctx) == 2
+    two = m2.forward_batch(ids)
+    assert np.array_equal(one, two)
+
+
+# SURVEY §8 configurations other than the bench's (C3): shapes at full size,
+# oracle parity on a few sentences, size-independent properties on the batch.
+SURVEY_CONFIGS = {
+    "C2-MiniLM-f16-L128-B32": ("all-MiniLM-L6-v2", "f16", [128] * 32, [0, 31]),
+    "C4-bge-large-q4_1-L512-B32-shard": ("bge-large-en-v1.5", "q4_1", [512] * 32, [5]),
+    "C5-bge-base-zh-q8_0-ragged-B128": ("bge-base-zh-v1.5", "q8_0",
+                                        list(np.random.default_rng(11).integers(16, 513, 128)), None),
+}
+
+
+@pytest.mark.parametrize("cfg", list(SURVEY_CONFIGS))
+def test_survey_config(tmp_path, cfg):
+    arch, ftype, lens, check = SURVEY_CONFIGS[cfg]
+    hp = bertpy.ARCHS[arch]
+    path = str(tmp_path / f"{arch}-{ftype}.bin")
+    bertpy.synthetic_model(path, arch, ftype, seed=1234)
+    m = bertpy.BertModel(path)
+    ids = bertpy.synthetic_ids(len(lens), lens, hp["n_vocab"], seed=7)
+    full = m.forward_batch(ids)
+    assert np.all(np.isfinite(full))
+    assert np.allclose(np.linalg.norm(full, axis=1), 1.0, atol=1e-5)
+    if check is None:                            # ragged: shortest and longest
+        check = [int(np.argmin(lens)), int(np.argmax(lens))]
+    sub = m.forward_batch([ids[i] for i in check])
+    assert np.array_equal(sub, full[check])      # batch-composition invariance
+    ref = oracle_lib.Oracle(path).forward_batch([ids[i] for i in check], n_threads=min(16, os.cpu_count() or 1))
+    c = cosines(full[check], ref)
+    print(cfg, "min cos vs oracle", c.min())
+    assert np.all(c >= 1 - COS_TOL), c
