@@ -17,14 +17,19 @@ namespace emb {
 
 template <int DH>
 __global__ __launch_bounds__(256) void attention_kernel(const h16 *__restrict__ qkv, const int32_t *__restrict__ cu,
-                                                        int d, float sl2, h16 *__restrict__ out)
+                                                        int d, int nqt, int nh, float sl2, h16 *__restrict__ out)
 {
     constexpr int KT = 64, KSTR = DH + 8, VSTR = KT + 8;
     __shared__ __attribute__((aligned(16))) h16 Ks[KT * KSTR];
     __shared__ __attribute__((aligned(16))) h16 Vt[DH * VSTR];
-    const int b = blockIdx.z, h = blockIdx.y;
+    // XCD-aware order: the query tiles of one (sentence, head) get consecutive
+    // logical ids on ONE XCD, so its K/V tiles are fetched into that XCD's L2
+    // once instead of once per XCD (dispatch is round-robin over the 8 XCDs).
+    const int nb = gridDim.x, bid = blockIdx.x, xcd = bid & 7, qq = nb >> 3, rr = nb & 7;
+    const int t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+    const int qt = t % nqt, h = (t / nqt) % nh, b = t / (nqt * nh);
     const int start = cu[b], len = cu[b + 1] - start;
-    const int q0 = blockIdx.x * ATT_QT;
+    const int q0 = qt * ATT_QT;
     if (q0 >= len) return;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int hi = lane >> 5, lq = lane & 31;
@@ -145,11 +150,12 @@ void launch_attention(const uint16_t *qkv, const int32_t *cu, int32_t n_seqs, in
 {
     const int dh = d / n_head;
     const float sl2 = (1.0f / sqrtf((float)dh)) * 1.4426950408889634f;
-    dim3 grid((max_len + ATT_QT - 1) / ATT_QT, n_head, n_seqs);
+    const int nqt = (max_len + ATT_QT - 1) / ATT_QT;
+    const int grid = nqt * n_head * n_seqs;
     if (dh == 64)
-        attention_kernel<64><<<grid, 256, 0, s>>>((const h16 *)qkv, cu, d, sl2, (h16 *)out);
+        attention_kernel<64><<<grid, 256, 0, s>>>((const h16 *)qkv, cu, d, nqt, n_head, sl2, (h16 *)out);
     else
-        attention_kernel<32><<<grid, 256, 0, s>>>((const h16 *)qkv, cu, d, sl2, (h16 *)out);
+        attention_kernel<32><<<grid, 256, 0, s>>>((const h16 *)qkv, cu, d, nqt, n_head, sl2, (h16 *)out);
 }
 
 }  // namespace emb
