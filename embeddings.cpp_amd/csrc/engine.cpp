@@ -565,10 +565,42 @@ extern "C" int32_t bertx_bench_gemm(int32_t fmt, int32_t N, int32_t K, int32_t M
                                  tile_n ? tile_n : 256);
         else {
             g_force_bn = tile_n;
+            g_gemm_variant = ablate == -2 ? 1 : ablate == -4 ? 2 : 0;   // -2: gemmq (2 x 4), -4: gemmqw
             launch_gemm(W, (const uint16_t *)dx, Mp, (const float *)db, epi, (const float *)dr, dout, nullptr);
             g_force_bn = 0;
+            g_gemm_variant = 0;
         }
     };
+    if (ablate == -3 && fdev == FMT_Q4_0) {
+        // stamped diagnostics: one launch, per-wave phase cycles to stderr
+        const int wm = tile_n == 128 ? 2 : 1;
+        const int nt = (Mp / GEMM_BM) * ((N + 256 / wm - 1) / (256 / wm));
+        uint64_t *dst = nullptr;
+        HIP_RC(hipMalloc((void **)&dst, (size_t)nt * 32 * 8));
+        for (int i = 0; i < 3; ++i) launch_gemm_q_stamped(W, (const uint16_t *)dx, Mp, (const float *)db, epi,
+                                                          (const float *)dr, dout, nullptr, wm, dst);
+        HIP_RC(hipDeviceSynchronize());
+        std::vector<uint64_t> h((size_t)nt * 32);
+        HIP_RC(hipMemcpy(h.data(), dst, h.size() * 8, hipMemcpyDeviceToHost));
+        (void)hipFree(dst);
+        std::vector<double> pro, loop, epi_c, wg;
+        uint64_t t0 = ~0ull, t1 = 0;
+        for (int b = 0; b < nt; ++b)
+            for (int w = 0; w < 8; ++w) {
+                const uint64_t *p = &h[((size_t)b * 8 + w) * 4];
+                if (!p[3]) continue;
+                pro.push_back((double)(p[1] - p[0]));
+                loop.push_back((double)(p[2] - p[1]) / (K / 64));
+                epi_c.push_back((double)(p[3] - p[2]));
+                wg.push_back((double)(p[3] - p[0]));
+                t0 = std::min(t0, p[0]);
+                t1 = std::max(t1, p[3]);
+            }
+        auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v.empty() ? 0.0 : v[v.size() / 2]; };
+        std::fprintf(stderr, "stamps N=%d K=%d M=%d wm=%d: tiles %d  median cycles: prologue %.0f  per-K-step %.0f  "
+                     "epilogue %.0f  wave total %.0f  | kernel span %.0f\n", N, K, Mp, wm, nt, med(pro), med(loop),
+                     med(epi_c), med(wg), (double)(t1 - t0));
+    }
     for (int i = 0; i < 3; ++i) launch();
     hipEvent_t a, b;
     HIP_RC(hipEventCreate(&a));

@@ -317,6 +317,394 @@ __global__ __launch_bounds__(512, 1) void gemmq_kernel(DevWeight W, const h16 *_
     }
 }
 
+// ---------------------------------------------------------------------------
+// gemmqw: the same contraction with the 8 waves laid out along the FEATURES.
+// Tile 256 tokens x BN features, BN = 32 * 8 / WM; wave w owns features
+// n0 + 32*(w % (8/WM)) .. +31 and tokens (w / (8/WM)) * 256/WM .. +256/WM-1.
+// Every A fragment (dequantized weights) therefore feeds 256/WM/32 MFMAs
+// (8 at WM = 1: half the dequant VALU per MFMA of the 2 x 4 layout) and each
+// weight byte is loaded by exactly one wave.  Weights: a 3-set register ring,
+// two K-steps ahead; X: 3-stage LDS-DMA ring, two K-steps ahead; one barrier
+// per K-step.  Epilogue straight from the accumulators (no LDS staging):
+// f16 rows widened to 16-B stores with v_permlane32_swap, f32 rows as 16-B
+// runs of 4 features.
+// ---------------------------------------------------------------------------
+template <int FMT, int EPI, int WM, bool STAMP = false>
+__global__ __launch_bounds__(512, 1) void gemmqw_kernel(DevWeight W, const h16 *__restrict__ X,
+                                                        const float *__restrict__ bias, const float *__restrict__ res,
+                                                        void *__restrict__ out, int nN, int nTiles,
+                                                        uint64_t *__restrict__ stamps = nullptr)
+{
+    // STAMP (diagnostics build only): s_memtime at start / after the prologue /
+    // after the K loop / after the epilogue, per wave, into stamps[]
+    uint64_t ts[4];
+    if constexpr (STAMP) ts[0] = __builtin_amdgcn_s_memtime();
+    constexpr int WN = 8 / WM;                 // waves along the features
+    constexpr int BN = 32 * WN;                // 256 (WM 1) or 128 (WM 2)
+    constexpr int TM = GM / WM;                // tokens per wave
+    constexpr int NJ = TM / 32;                // B fragments (32-token groups) per k-slice
+    constexpr int QB = FMT == FMT_Q8_0 ? 64 : 32;
+    constexpr int P = QRegs<FMT>::LOADS + 4;   // vector-memory ops issued per K-step per wave
+    __shared__ __attribute__((aligned(16))) char smem[XS * X_BYTES];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int b = blockIdx.x, xcd = b & 7, qq = nTiles >> 3, rr = nTiles & 7;
+    const int t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
+    const int m0 = (t / nN) * GM, n0 = (t % nN) * BN;
+    const int K = W.K, N = W.N, KS = K / GK;
+    const int wm = wave / WN, wn = wave % WN, lr = lane & 31, hi = lane >> 5;
+    const int nw = n0 + 32 * wn;               // this wave's first feature
+
+    const h16 *xp[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = 32 * wave + 8 * i + (lane >> 3);
+        xp[i] = X + (size_t)(m0 + r) * K + (((lane & 7) ^ ((r >> 1) & 7)) * 8);
+    }
+#define EMB_ISSUE_XW(ks_, stage_)                                                                   \
+    {                                                                                               \
+        char *dst_ = smem + (stage_) * X_BYTES + ((32 * wave) << 7);                                \
+        glds<16>(xp[0] + (ks_) * GK, dst_);                                                         \
+        glds<16>(xp[1] + (ks_) * GK, dst_ + (8 << 7));                                              \
+        glds<16>(xp[2] + (ks_) * GK, dst_ + (16 << 7));                                             \
+        glds<16>(xp[3] + (ks_) * GK, dst_ + (24 << 7));                                             \
+    }
+    const int nrow = min(nw + lr, N - 1);
+    const uint8_t *wq = (const uint8_t *)W.qs + (size_t)nrow * QB + (QB / 2) * hi;
+    const uint32_t *wd = (const uint32_t *)W.d + nrow;
+    const uint32_t *wmn = FMT == FMT_Q4_1 ? (const uint32_t *)W.m + nrow : nullptr;
+    const size_t qstep = (size_t)N * QB, sstep = (size_t)N;
+
+    f32x16 acc[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+
+    // prologue: W(0), X(0), W(1), X(1) in flight; retire W(0), X(0)
+    QRegs<FMT> w0, w1, w2;
+    const int k1 = min(1, KS - 1);
+    w0.load(wq, wd, wmn);
+    EMB_ISSUE_XW(0, 0)
+    w1.load(wq + k1 * qstep, wd + k1 * sstep, FMT == FMT_Q4_1 ? wmn + k1 * sstep : nullptr);
+    EMB_ISSUE_XW(k1, 1)
+    wait_vmcnt<P>();
+    lds_barrier();
+    if constexpr (STAMP) ts[1] = __builtin_amdgcn_s_memtime();
+
+    const int sw = (lr >> 1) & 7;
+    const int rbase = (wm * TM + lr) << 7;
+    int st = 0;
+
+// One K-step with CUR's weights: W(ks+2) -> NXT2, X(ks+2) -> its stage (clamped:
+// past the end the issues re-read step KS-1), explicit no-op wait declaring CUR
+// landed, MFMAs, then retire step ks+1's operands and barrier.
+#define EMB_WSTEP(CUR, NXT2, ks_)                                                                         \
+    {                                                                                                     \
+        const int ksx = (ks_);                                                                            \
+        const int st2 = st == 0 ? 2 : st - 1;                                                             \
+        {                                                                                                 \
+            const int k2 = min(ksx + 2, KS - 1);                                                          \
+            NXT2.load(wq + k2 * qstep, wd + k2 * sstep, FMT == FMT_Q4_1 ? wmn + k2 * sstep : nullptr);    \
+            EMB_ISSUE_XW(k2, st2)                                                                         \
+            wait_vmcnt<2 * P>();                                                                          \
+            CUR.pin_all();                                                                                \
+        }                                                                                                 \
+        const char *xs = smem + st * X_BYTES + rbase;                                                     \
+        _Pragma("unroll") for (int kk = 0; kk < 4; ++kk)                                                  \
+        {                                                                                                 \
+            const int cx = ((2 * kk + hi) ^ sw) << 4;                                                     \
+            h16x8 bf[NJ];                                                                                 \
+            _Pragma("unroll") for (int j = 0; j < NJ; ++j) bf[j] = *(const h16x8 *)(xs + (j << 12) + cx); \
+            const h16x8 a = CUR.frag(kk);                                                                 \
+            _Pragma("unroll") for (int j = 0; j < NJ; ++j) acc[j] =                                       \
+                __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bf[j], acc[j], 0, 0, 0);                        \
+        }                                                                                                 \
+        wait_vmcnt<P>(); /* step ks+1's W and X landed; step ks+2's may fly */                           \
+        lds_barrier();                                                                                    \
+        st = st == 2 ? 0 : st + 1;                                                                        \
+    }
+
+    // whole triples in the loop (no guarded steps: a guard is a path on which
+    // the compiler's waitcnt model loses track and drains with vmcnt(0)), then
+    // the 0-2 remaining steps
+    int ks = 0;
+    for (; ks + 3 <= KS; ks += 3) {
+        EMB_WSTEP(w0, w2, ks)
+        EMB_WSTEP(w1, w0, ks + 1)
+        EMB_WSTEP(w2, w1, ks + 2)
+    }
+    if (ks < KS) {
+        EMB_WSTEP(w0, w2, ks)
+        if (ks + 1 < KS) EMB_WSTEP(w1, w0, ks + 1)
+    }
+#undef EMB_WSTEP
+#undef EMB_ISSUE_XW
+    wait_vmcnt<0>();   // the clamped tail re-reads still write LDS / registers
+    if constexpr (STAMP) ts[2] = __builtin_amdgcn_s_memtime();
+
+    // ---- epilogue: lane holds token 32j + lr, features nw + 8g + 4hi + e ----
+    if (nw >= N) return;                       // wave-uniform (N % 32 == 0)
+    const int mrow = m0 + wm * TM + lr;
+    f32x4 bb[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) bb[g] = *(const f32x4 *)(bias + nw + 8 * g + 4 * hi);
+    if constexpr (EPI == EPI_BIAS_RES_F32) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const size_t rowo = (size_t)(mrow + 32 * j) * N + nw + 4 * hi;
+            f32x4 rv[4];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) rv[g] = *(const f32x4 *)(res + rowo + 8 * g);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                f32x4 o;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[e] = rv[g][e] + (bb[g][e] + acc[j][4 * g + e]);
+                *(f32x4 *)((float *)out + rowo + 8 * g) = o;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            uint32_t pk[4][2];                 // group g: 4 f16 of features 8g + 4hi + 0..3
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                h16 o[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float v = bb[g][e] + acc[j][4 * g + e];
+                    o[e] = EPI == EPI_BIAS_GELU_F16 ? gelu_era(v) : (h16)v;
+                }
+                pk[g][0] = __builtin_bit_cast(uint32_t, h16x2{o[0], o[1]});
+                pk[g][1] = __builtin_bit_cast(uint32_t, h16x2{o[2], o[3]});
+            }
+            // T21: half-exchange pairs (g, g+1) -> lanes 0-31 hold features 8g..8g+7,
+            // lanes 32-63 hold 8g+8..8g+15 of the same token
+            h16 *orow = (h16 *)out + (size_t)(mrow + 32 * j) * N + nw + 8 * hi;
+#pragma unroll
+            for (int g = 0; g < 4; g += 2) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const auto r2 = __builtin_amdgcn_permlane32_swap(pk[g][h], pk[g + 1][h], false, false);
+                    pk[g][h] = r2[0];
+                    pk[g + 1][h] = r2[1];
+                }
+                uint4 v;
+                v.x = pk[g][0]; v.y = pk[g][1]; v.z = pk[g + 1][0]; v.w = pk[g + 1][1];
+                *(uint4 *)(orow + 8 * g) = v;
+            }
+        }
+    }
+    if constexpr (STAMP) {
+        ts[3] = __builtin_amdgcn_s_memtime();
+        if (lane == 0)
+            for (int i = 0; i < 4; ++i) stamps[((size_t)blockIdx.x * 8 + wave) * 4 + i] = ts[i];
+    }
+}
+
+template <int FMT, int WM, bool STAMP = false>
+void dispatch_qw(const DevWeight &W, const h16 *x, int M, const float *bias, int epi, const float *res, void *out,
+                 hipStream_t s, uint64_t *stamps = nullptr)
+{
+    constexpr int BN = 256 / WM;
+    const int nN = (W.N + BN - 1) / BN, nTiles = (M / GM) * nN;
+    if (epi == EPI_BIAS_F16)
+        gemmqw_kernel<FMT, EPI_BIAS_F16, WM, STAMP><<<nTiles, 512, 0, s>>>(W, x, bias, res, out, nN, nTiles, stamps);
+    else if (epi == EPI_BIAS_GELU_F16)
+        gemmqw_kernel<FMT, EPI_BIAS_GELU_F16, WM, STAMP><<<nTiles, 512, 0, s>>>(W, x, bias, res, out, nN, nTiles,
+                                                                              stamps);
+    else
+        gemmqw_kernel<FMT, EPI_BIAS_RES_F32, WM, STAMP><<<nTiles, 512, 0, s>>>(W, x, bias, res, out, nN, nTiles,
+                                                                             stamps);
+}
+
+// ---------------------------------------------------------------------------
+// gemmqv: TWO workgroups per CU.  4 waves (256 threads) per workgroup, tile
+// BM tokens x 128 features, wave w owns features n0 + 32w .. +31 and all BM
+// tokens (NJ = BM/32 B fragments per k-slice).  Two independent workgroups per
+// CU drift apart, so one's epilogue (HBM store burst, GELU VALU) and prologue
+// overlap the other's MFMA loop -- with one workgroup per CU every CU hit its
+// epilogue at the same moment (measured: 30-40 % of the tile time).
+// X: 2-stage LDS-DMA ring (64 KiB at BM 256), one K-step ahead; W: 3-set
+// register ring, two K-steps ahead; one barrier per K-step.
+// ---------------------------------------------------------------------------
+template <int FMT, int EPI, int BM>
+__global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemmqv_kernel(DevWeight W, const h16 *__restrict__ X,
+                                                        const float *__restrict__ bias, const float *__restrict__ res,
+                                                        void *__restrict__ out, int nN, int nTiles)
+{
+    constexpr int BN = 128;
+    constexpr int NJ = BM / 32;
+    constexpr int XB = BM * GK * 2;            // bytes per X stage
+    constexpr int XG = XB / (256 * 16);        // LDS-DMA instructions per wave per stage
+    constexpr int QB = FMT == FMT_Q8_0 ? 64 : 32;
+    constexpr int LQ = QRegs<FMT>::LOADS;
+    __shared__ __attribute__((aligned(16))) char smem[2 * XB];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int b = blockIdx.x, xcd = b & 7, qq = nTiles >> 3, rr = nTiles & 7;
+    const int t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
+    const int m0 = (t / nN) * BM, n0 = (t % nN) * BN;
+    const int K = W.K, N = W.N, KS = K / GK;
+    const int lr = lane & 31, hi = lane >> 5;
+    const int nw = n0 + 32 * wave;
+
+    // X LDS-DMA sources: XG instructions per wave, rows (XG*8)*wave + 8i + lane/8
+    const h16 *xp[XG];
+#pragma unroll
+    for (int i = 0; i < XG; ++i) {
+        const int r = 8 * XG * wave + 8 * i + (lane >> 3);
+        xp[i] = X + (size_t)(m0 + r) * K + (((lane & 7) ^ ((r >> 1) & 7)) * 8);
+    }
+#define EMB_ISSUE_XV(ks_, stage_)                                                                   \
+    {                                                                                               \
+        char *dst_ = smem + (stage_) * XB + ((8 * XG * wave) << 7);                                 \
+        _Pragma("unroll") for (int i = 0; i < XG; ++i) glds<16>(xp[i] + (ks_) * GK, dst_ + (i << 10)); \
+    }
+    const int nrow = min(nw + lr, N - 1);
+    const uint8_t *wq = (const uint8_t *)W.qs + (size_t)nrow * QB + (QB / 2) * hi;
+    const uint32_t *wd = (const uint32_t *)W.d + nrow;
+    const uint32_t *wmn = FMT == FMT_Q4_1 ? (const uint32_t *)W.m + nrow : nullptr;
+    const size_t qstep = (size_t)N * QB, sstep = (size_t)N;
+
+    f32x16 acc[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+
+    // prologue: W(0), X(0) -> stage 0, W(1); retire W(0) and X(0)
+    QRegs<FMT> w0, w1, w2;
+    const int k1 = min(1, KS - 1);
+    w0.load(wq, wd, wmn);
+    EMB_ISSUE_XV(0, 0)
+    w1.load(wq + k1 * qstep, wd + k1 * sstep, FMT == FMT_Q4_1 ? wmn + k1 * sstep : nullptr);
+    wait_vmcnt<LQ>();
+    lds_barrier();
+
+    const int sw = (lr >> 1) & 7;
+    const int rbase = lr << 7;
+    int st = 0;
+
+// One K-step with CUR's weights: X(ks+1) -> the other stage, W(ks+2) -> NXT2
+// (clamped past the end), explicit no-op wait declaring CUR landed, MFMAs, then
+// retire X(ks+1) and W(ks+1) (everything but W(ks+2)) and barrier.
+#define EMB_VSTEP(CUR, NXT2, ks_)                                                                         \
+    {                                                                                                     \
+        const int ksx = (ks_);                                                                            \
+        {                                                                                                 \
+            const int kx = min(ksx + 1, KS - 1), k2 = min(ksx + 2, KS - 1);                               \
+            EMB_ISSUE_XV(kx, st ^ 1)                                                                      \
+            asm volatile("" ::: "memory"); /* keep X(ks+1) older than W(ks+2): the end wait splits them */ \
+            NXT2.load(wq + k2 * qstep, wd + k2 * sstep, FMT == FMT_Q4_1 ? wmn + k2 * sstep : nullptr);    \
+            wait_vmcnt<2 * LQ + XG>();                                                                    \
+            CUR.pin_all();                                                                                \
+        }                                                                                                 \
+        const char *xs = smem + st * XB + rbase;                                                          \
+        h16x8 bf[NJ], bn[NJ];                                                                             \
+        _Pragma("unroll") for (int j = 0; j < NJ; ++j) bf[j] = *(const h16x8 *)(xs + (j << 12) + (hi ^ sw) * 16); \
+        _Pragma("unroll") for (int kk = 0; kk < 4; ++kk)                                                  \
+        {                                                                                                 \
+            if (kk < 3) {                                                                                 \
+                const int cx = ((2 * kk + 2 + hi) ^ sw) << 4;                                             \
+                _Pragma("unroll") for (int j = 0; j < NJ; ++j) bn[j] = *(const h16x8 *)(xs + (j << 12) + cx); \
+            }                                                                                             \
+            const h16x8 a = CUR.frag(kk);                                                                 \
+            _Pragma("unroll") for (int j = 0; j < NJ; ++j) acc[j] =                                       \
+                __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bf[j], acc[j], 0, 0, 0);                        \
+            if (kk < 3) {                                                                                 \
+                _Pragma("unroll") for (int j = 0; j < NJ; ++j) bf[j] = bn[j];                             \
+            }                                                                                             \
+        }                                                                                                 \
+        wait_vmcnt<LQ>(); /* X(ks+1), W(ks+1) landed; W(ks+2) may fly */                                 \
+        lds_barrier();                                                                                    \
+        st ^= 1;                                                                                          \
+    }
+
+    int ks = 0;
+    for (; ks + 3 <= KS; ks += 3) {
+        EMB_VSTEP(w0, w2, ks)
+        EMB_VSTEP(w1, w0, ks + 1)
+        EMB_VSTEP(w2, w1, ks + 2)
+    }
+    if (ks < KS) {
+        EMB_VSTEP(w0, w2, ks)
+        if (ks + 1 < KS) EMB_VSTEP(w1, w0, ks + 1)
+    }
+#undef EMB_VSTEP
+#undef EMB_ISSUE_XV
+    wait_vmcnt<0>();
+
+    // ---- epilogue: lane holds token m0 + 32j + lr, features nw + 8g + 4hi + e ----
+    if (nw >= N) return;                       // wave-uniform (N % 32 == 0)
+    const int mrow = m0 + lr;
+    f32x4 bb[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) bb[g] = *(const f32x4 *)(bias + nw + 8 * g + 4 * hi);
+    if constexpr (EPI == EPI_BIAS_RES_F32) {
+        f32x4 rv[NJ][4];                       // all residual loads in flight at once
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+                rv[j][g] = *(const f32x4 *)(res + (size_t)(mrow + 32 * j) * N + nw + 4 * hi + 8 * g);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const size_t rowo = (size_t)(mrow + 32 * j) * N + nw + 4 * hi;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                f32x4 o;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[e] = rv[j][g][e] + (bb[g][e] + acc[j][4 * g + e]);
+                *(f32x4 *)((float *)out + rowo + 8 * g) = o;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            uint32_t pk[4][2];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                h16 o[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float v = bb[g][e] + acc[j][4 * g + e];
+                    o[e] = EPI == EPI_BIAS_GELU_F16 ? gelu_era(v) : (h16)v;
+                }
+                pk[g][0] = __builtin_bit_cast(uint32_t, h16x2{o[0], o[1]});
+                pk[g][1] = __builtin_bit_cast(uint32_t, h16x2{o[2], o[3]});
+            }
+            h16 *orow = (h16 *)out + (size_t)(mrow + 32 * j) * N + nw + 8 * hi;
+#pragma unroll
+            for (int g = 0; g < 4; g += 2) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const auto r2 = __builtin_amdgcn_permlane32_swap(pk[g][h], pk[g + 1][h], false, false);
+                    pk[g][h] = r2[0];
+                    pk[g + 1][h] = r2[1];
+                }
+                uint4 v;
+                v.x = pk[g][0]; v.y = pk[g][1]; v.z = pk[g + 1][0]; v.w = pk[g + 1][1];
+                *(uint4 *)(orow + 8 * g) = v;
+            }
+        }
+    }
+}
+
+template <int FMT, int BM>
+void dispatch_qv(const DevWeight &W, const h16 *x, int M, const float *bias, int epi, const float *res, void *out,
+                 hipStream_t s)
+{
+    const int nN = (W.N + 127) / 128, nTiles = (M / BM) * nN;
+    if (epi == EPI_BIAS_F16)
+        gemmqv_kernel<FMT, EPI_BIAS_F16, BM><<<nTiles, 256, 0, s>>>(W, x, bias, res, out, nN, nTiles);
+    else if (epi == EPI_BIAS_GELU_F16)
+        gemmqv_kernel<FMT, EPI_BIAS_GELU_F16, BM><<<nTiles, 256, 0, s>>>(W, x, bias, res, out, nN, nTiles);
+    else
+        gemmqv_kernel<FMT, EPI_BIAS_RES_F32, BM><<<nTiles, 256, 0, s>>>(W, x, bias, res, out, nN, nTiles);
+}
+
 template <int FMT, int BN>
 void dispatch_q_bn(const DevWeight &W, const h16 *x, int M, const float *bias, int epi, const float *res, void *out,
                    hipStream_t s)
@@ -332,10 +720,68 @@ void dispatch_q_bn(const DevWeight &W, const h16 *x, int M, const float *bias, i
 
 }  // namespace
 
+// Diagnostics: q4_0 gemmqw with per-wave s_memtime stamps (4 per wave) into `stamps`
+// (device buffer of nTiles * 8 * 4 uint64).  Returns the tile count.
+int launch_gemm_q_stamped(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi,
+                          const float *res, void *out, hipStream_t s, int32_t wm, uint64_t *stamps)
+{
+    const h16 *x = (const h16 *)X;
+    const int BN = 256 / wm;
+    if (wm == 1) dispatch_qw<FMT_Q4_0, 1, true>(W, x, M, bias, epi, res, out, s, stamps);
+    else dispatch_qw<FMT_Q4_0, 2, true>(W, x, M, bias, epi, res, out, s, stamps);
+    return (M / GM) * ((W.N + BN - 1) / BN);
+}
+
+int g_gemm_variant = 0;   // 0: gemmqv (2 WG/CU), 1: gemmq (2 x 4 waves), 2: gemmqw -- A/B benches
+
 void launch_gemm_q(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi, const float *res,
                    void *out, hipStream_t s, int32_t force_bn)
 {
     const h16 *x = (const h16 *)X;
+    int variant = g_gemm_variant;
+    // measured (profiles/r01_gemm_sweep.log): the GELU form is fastest as gemmqw
+    // (one 8-wave workgroup per CU), the others as gemmqv (two per CU)
+    if (variant == 0 && epi == EPI_BIAS_GELU_F16 && !force_bn && W.N % 256 == 0 &&
+        (long)(M / GM) * (W.N / 256) >= 512)
+        variant = 2;
+    if (variant == 0) {
+        // 2 workgroups / CU; BM 128 for the residual (f32) form and for small M
+        const bool big = force_bn ? force_bn == 256 : (epi != EPI_BIAS_RES_F32 && M >= 256 * 64);
+        switch (W.fmt) {
+        case FMT_Q4_0:
+            if (big) dispatch_qv<FMT_Q4_0, 256>(W, x, M, bias, epi, res, out, s);
+            else dispatch_qv<FMT_Q4_0, 128>(W, x, M, bias, epi, res, out, s);
+            break;
+        case FMT_Q4_1:
+            if (big) dispatch_qv<FMT_Q4_1, 256>(W, x, M, bias, epi, res, out, s);
+            else dispatch_qv<FMT_Q4_1, 128>(W, x, M, bias, epi, res, out, s);
+            break;
+        default:
+            if (big) dispatch_qv<FMT_Q8_0, 256>(W, x, M, bias, epi, res, out, s);
+            else dispatch_qv<FMT_Q8_0, 128>(W, x, M, bias, epi, res, out, s);
+            break;
+        }
+        return;
+    }
+    if (variant == 2) {
+        const bool wide = force_bn ? force_bn == 256
+                                   : (W.N % 256 == 0 && (long)(M / GM) * (W.N / 256) >= 512);
+        switch (W.fmt) {
+        case FMT_Q4_0:
+            if (wide) dispatch_qw<FMT_Q4_0, 1>(W, x, M, bias, epi, res, out, s);
+            else dispatch_qw<FMT_Q4_0, 2>(W, x, M, bias, epi, res, out, s);
+            break;
+        case FMT_Q4_1:
+            if (wide) dispatch_qw<FMT_Q4_1, 1>(W, x, M, bias, epi, res, out, s);
+            else dispatch_qw<FMT_Q4_1, 2>(W, x, M, bias, epi, res, out, s);
+            break;
+        default:
+            if (wide) dispatch_qw<FMT_Q8_0, 1>(W, x, M, bias, epi, res, out, s);
+            else dispatch_qw<FMT_Q8_0, 2>(W, x, M, bias, epi, res, out, s);
+            break;
+        }
+        return;
+    }
     const bool wide = force_bn ? (force_bn == 256 && epi != EPI_BIAS_RES_F32 && W.N % 256 == 0)
                                : (epi != EPI_BIAS_RES_F32 && W.N % 256 == 0 && (long)(M / GM) * (W.N / 256) >= 512);
     switch (W.fmt) {

@@ -60,6 +60,11 @@ void launch_gemm_q(const DevWeight &W, const uint16_t *X, int32_t M, const float
 
 // Tests only: force the GEMM tile width (128 / 256; 0 = heuristic).
 extern int g_force_bn;
+// Benches only: quantized GEMM kernel variant (0 = gemmqw, 1 = gemmq).
+extern int g_gemm_variant;
+// Diagnostics: q4_0 gemmqw (wm waves along tokens) with per-wave s_memtime stamps.
+int launch_gemm_q_stamped(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi,
+                          const float *res, void *out, hipStream_t s, int32_t wm, uint64_t *stamps);
 
 // Diagnostics only: q4_0 GEMM with parts switched off (1 no per-step loads,
 // 2 no dequant, 4 no MFMA, 8 no epilogue; combinations 3, 6, 11, 15).
