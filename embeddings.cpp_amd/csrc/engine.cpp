@@ -571,14 +571,16 @@ extern "C" int32_t bertx_bench_gemm(int32_t fmt, int32_t N, int32_t K, int32_t M
             g_gemm_variant = 0;
         }
     };
-    if (ablate == -3 && fdev == FMT_Q4_0) {
+    if (ablate <= -3 && ablate >= -40 && fdev == FMT_Q4_0) {
+        // -3: stamps; -3 - d: stamps + ablation d of gemmqw (kernels.h)
+        const int diag = -3 - ablate;
         // stamped diagnostics: one launch, per-wave phase cycles to stderr
         const int wm = tile_n == 128 ? 2 : 1;
         const int nt = (Mp / GEMM_BM) * ((N + 256 / wm - 1) / (256 / wm));
         uint64_t *dst = nullptr;
         HIP_RC(hipMalloc((void **)&dst, (size_t)nt * 32 * 8));
         for (int i = 0; i < 3; ++i) launch_gemm_q_stamped(W, (const uint16_t *)dx, Mp, (const float *)db, epi,
-                                                          (const float *)dr, dout, nullptr, wm, dst);
+                                                          (const float *)dr, dout, nullptr, wm, dst, diag);
         HIP_RC(hipDeviceSynchronize());
         std::vector<uint64_t> h((size_t)nt * 32);
         HIP_RC(hipMemcpy(h.data(), dst, h.size() * 8, hipMemcpyDeviceToHost));
@@ -597,8 +599,8 @@ extern "C" int32_t bertx_bench_gemm(int32_t fmt, int32_t N, int32_t K, int32_t M
                 t1 = std::max(t1, p[3]);
             }
         auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v.empty() ? 0.0 : v[v.size() / 2]; };
-        std::fprintf(stderr, "stamps N=%d K=%d M=%d wm=%d: tiles %d  median cycles: prologue %.0f  per-K-step %.0f  "
-                     "epilogue %.0f  wave total %.0f  | kernel span %.0f\n", N, K, Mp, wm, nt, med(pro), med(loop),
+        std::fprintf(stderr, "stamps diag=%d N=%d K=%d M=%d wm=%d: tiles %d  median cycles: prologue %.0f  per-K-step %.0f  "
+                     "epilogue %.0f  wave total %.0f  | kernel span %.0f\n", diag, N, K, Mp, wm, nt, med(pro), med(loop),
                      med(epi_c), med(wg), (double)(t1 - t0));
     }
     for (int i = 0; i < 3; ++i) launch();

@@ -329,7 +329,10 @@ __global__ __launch_bounds__(512, 1) void gemmq_kernel(DevWeight W, const h16 *_
 // f16 rows widened to 16-B stores with v_permlane32_swap, f32 rows as 16-B
 // runs of 4 features.
 // ---------------------------------------------------------------------------
-template <int FMT, int EPI, int WM, bool STAMP = false>
+// DIAG (diagnostics builds only): 0x10 stamps; ablations 0x1 no dequant (raw
+// words as A), 0x2 no B ds_reads (fragments from the prologue), 0x4 no barrier
+// in the K loop, 0x8 no MFMA.
+template <int FMT, int EPI, int WM, int DIAG = 0>
 __global__ __launch_bounds__(512, 1) void gemmqw_kernel(DevWeight W, const h16 *__restrict__ X,
                                                         const float *__restrict__ bias, const float *__restrict__ res,
                                                         void *__restrict__ out, int nN, int nTiles,
@@ -337,6 +340,7 @@ __global__ __launch_bounds__(512, 1) void gemmqw_kernel(DevWeight W, const h16 *
 {
     // STAMP (diagnostics build only): s_memtime at start / after the prologue /
     // after the K loop / after the epilogue, per wave, into stamps[]
+    constexpr bool STAMP = (DIAG & 0x10) != 0;
     uint64_t ts[4];
     if constexpr (STAMP) ts[0] = __builtin_amdgcn_s_memtime();
     constexpr int WN = 8 / WM;                 // waves along the features
@@ -395,6 +399,11 @@ __global__ __launch_bounds__(512, 1) void gemmqw_kernel(DevWeight W, const h16 *
     const int sw = (lr >> 1) & 7;
     const int rbase = (wm * TM + lr) << 7;
     int st = 0;
+    h16x8 bdiag[(DIAG & 0x2) ? NJ : 1];
+    if constexpr (DIAG & 0x2) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) bdiag[j] = *(const h16x8 *)(smem + rbase + (j << 12) + (hi << 4));
+    }
 
 // One K-step with CUR's weights: W(ks+2) -> NXT2, X(ks+2) -> its stage (clamped:
 // past the end the issues re-read step KS-1), explicit no-op wait declaring CUR
@@ -411,17 +420,54 @@ __global__ __launch_bounds__(512, 1) void gemmqw_kernel(DevWeight W, const h16 *
             CUR.pin_all();                                                                                \
         }                                                                                                 \
         const char *xs = smem + st * X_BYTES + rbase;                                                     \
+        if constexpr (DIAG & 0x20) {                                                                      \
+            /* software-pipelined: B fragments and A dequant of k-slice kk+1 issued */                   \
+            /* between the MFMAs of kk (sched_group_barrier pins the interleave) */                       \
+            h16x8 bc[NJ], bnx[NJ];                                                                        \
+            _Pragma("unroll") for (int j = 0; j < NJ; ++j) bc[j] = *(const h16x8 *)(xs + (j << 12) + ((hi ^ sw) << 4)); \
+            h16x8 ac = CUR.frag(0), anx;                                                                  \
+            _Pragma("unroll") for (int kk = 0; kk < 4; ++kk)                                              \
+            {                                                                                             \
+                if (kk < 3) {                                                                             \
+                    const int cx = ((2 * kk + 2 + hi) ^ sw) << 4;                                         \
+                    _Pragma("unroll") for (int j = 0; j < NJ; ++j) bnx[j] = *(const h16x8 *)(xs + (j << 12) + cx); \
+                    anx = CUR.frag(kk + 1);                                                               \
+                }                                                                                         \
+                _Pragma("unroll") for (int j = 0; j < NJ; ++j) acc[j] =                                   \
+                    __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bc[j], acc[j], 0, 0, 0);                   \
+                if (kk < 3) {                                                                             \
+                    _Pragma("unroll") for (int j = 0; j < NJ; ++j) {                                      \
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                \
+                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                \
+                        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);                                \
+                    }                                                                                     \
+                    _Pragma("unroll") for (int j = 0; j < NJ; ++j) bc[j] = bnx[j];                        \
+                    ac = anx;                                                                             \
+                }                                                                                         \
+            }                                                                                             \
+        } else                                                                                            \
         _Pragma("unroll") for (int kk = 0; kk < 4; ++kk)                                                  \
         {                                                                                                 \
             const int cx = ((2 * kk + hi) ^ sw) << 4;                                                     \
             h16x8 bf[NJ];                                                                                 \
-            _Pragma("unroll") for (int j = 0; j < NJ; ++j) bf[j] = *(const h16x8 *)(xs + (j << 12) + cx); \
-            const h16x8 a = CUR.frag(kk);                                                                 \
-            _Pragma("unroll") for (int j = 0; j < NJ; ++j) acc[j] =                                       \
-                __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bf[j], acc[j], 0, 0, 0);                        \
+            if constexpr (DIAG & 0x2) {                                                                   \
+                _Pragma("unroll") for (int j = 0; j < NJ; ++j) bf[j] = bdiag[j];                          \
+            } else {                                                                                      \
+                _Pragma("unroll") for (int j = 0; j < NJ; ++j) bf[j] = *(const h16x8 *)(xs + (j << 12) + cx); \
+            }                                                                                             \
+            h16x8 a;                                                                                      \
+            if constexpr (DIAG & 0x1) a = __builtin_bit_cast(h16x8, CUR.q);                               \
+            else a = CUR.frag(kk);                                                                        \
+            if constexpr (DIAG & 0x8) {                                                                   \
+                _Pragma("unroll") for (int j = 0; j < NJ; ++j) asm volatile("" :: "v"(a), "v"(bf[j]));   \
+            } else {                                                                                      \
+                _Pragma("unroll") for (int j = 0; j < NJ; ++j) acc[j] =                                   \
+                    __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bf[j], acc[j], 0, 0, 0);                    \
+            }                                                                                             \
         }                                                                                                 \
         wait_vmcnt<P>(); /* step ks+1's W and X landed; step ks+2's may fly */                           \
-        lds_barrier();                                                                                    \
+        if constexpr (DIAG & 0x4) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                     \
+        else lds_barrier();                                                                               \
         st = st == 2 ? 0 : st + 1;                                                                        \
     }
 
@@ -503,7 +549,7 @@ __global__ __launch_bounds__(512, 1) void gemmqw_kernel(DevWeight W, const h16 *
     }
 }
 
-template <int FMT, int WM, bool STAMP = false>
+template <int FMT, int WM, int STAMP = 0>
 void dispatch_qw(const DevWeight &W, const h16 *x, int M, const float *bias, int epi, const float *res, void *out,
                  hipStream_t s, uint64_t *stamps = nullptr)
 {
@@ -723,12 +769,25 @@ void dispatch_q_bn(const DevWeight &W, const h16 *x, int M, const float *bias, i
 // Diagnostics: q4_0 gemmqw with per-wave s_memtime stamps (4 per wave) into `stamps`
 // (device buffer of nTiles * 8 * 4 uint64).  Returns the tile count.
 int launch_gemm_q_stamped(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi,
-                          const float *res, void *out, hipStream_t s, int32_t wm, uint64_t *stamps)
+                          const float *res, void *out, hipStream_t s, int32_t wm, uint64_t *stamps, int32_t diag)
 {
     const h16 *x = (const h16 *)X;
     const int BN = 256 / wm;
-    if (wm == 1) dispatch_qw<FMT_Q4_0, 1, true>(W, x, M, bias, epi, res, out, s, stamps);
-    else dispatch_qw<FMT_Q4_0, 2, true>(W, x, M, bias, epi, res, out, s, stamps);
+    if (wm == 1) {
+        switch (diag) {
+        case 1: dispatch_qw<FMT_Q4_0, 1, 0x11>(W, x, M, bias, epi, res, out, s, stamps); break;
+        case 2: dispatch_qw<FMT_Q4_0, 1, 0x12>(W, x, M, bias, epi, res, out, s, stamps); break;
+        case 3: dispatch_qw<FMT_Q4_0, 1, 0x13>(W, x, M, bias, epi, res, out, s, stamps); break;
+        case 4: dispatch_qw<FMT_Q4_0, 1, 0x14>(W, x, M, bias, epi, res, out, s, stamps); break;
+        case 8: dispatch_qw<FMT_Q4_0, 1, 0x18>(W, x, M, bias, epi, res, out, s, stamps); break;
+        case 15: dispatch_qw<FMT_Q4_0, 1, 0x1f>(W, x, M, bias, epi, res, out, s, stamps); break;
+        case 32: dispatch_qw<FMT_Q4_0, 1, 0x30>(W, x, M, bias, epi, res, out, s, stamps); break;
+        case 36: dispatch_qw<FMT_Q4_0, 1, 0x34>(W, x, M, bias, epi, res, out, s, stamps); break;
+        default: dispatch_qw<FMT_Q4_0, 1, 0x10>(W, x, M, bias, epi, res, out, s, stamps); break;
+        }
+    } else {
+        dispatch_qw<FMT_Q4_0, 2, 0x10>(W, x, M, bias, epi, res, out, s, stamps);
+    }
     return (M / GM) * ((W.N + BN - 1) / BN);
 }
 

@@ -64,7 +64,8 @@ extern int g_force_bn;
 extern int g_gemm_variant;
 // Diagnostics: q4_0 gemmqw (wm waves along tokens) with per-wave s_memtime stamps.
 int launch_gemm_q_stamped(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi,
-                          const float *res, void *out, hipStream_t s, int32_t wm, uint64_t *stamps);
+                          const float *res, void *out, hipStream_t s, int32_t wm, uint64_t *stamps,
+                          int32_t diag);
 
 // Diagnostics only: q4_0 GEMM with parts switched off (1 no per-step loads,
 // 2 no dequant, 4 no MFMA, 8 no epilogue; combinations 3, 6, 11, 15).
