@@ -80,7 +80,9 @@ void repack_linear(const std::vector<const HostTensor *> &parts, int fmt_dev, Pi
                     uint16_t h;
                     if (t->fmt == FMT_F16) std::memcpy(&h, src + 2 * k, 2);
                     else { float f; std::memcpy(&f, src + 4 * k, 4); h = f32_to_f16(f); }
-                    dst[((size_t)(k / 64) * N + n) * 64 + (k % 64)] = h;
+                    // A-fragment order (kernels.h): k = 16kk + 8hh + i -> 32hh + 8kk + i
+                    const int kr = k % 64, kk = kr / 16, hh = (kr / 8) & 1, i = kr % 8;
+                    dst[((size_t)(k / 64) * N + n) * 64 + 32 * hh + 8 * kk + i] = h;
                 }
             }
         }
@@ -560,16 +562,11 @@ extern "C" int32_t bertx_bench_gemm(int32_t fmt, int32_t N, int32_t K, int32_t M
     W.fmt = fdev; W.N = N; W.K = K;
     W.qs = dq; W.d = (const uint16_t *)dd; W.m = (const uint16_t *)dd;
     auto launch = [&]() {
-        if (ablate >= 0 && fdev == FMT_F16)
-            launch_gemm_ablation(W, (const uint16_t *)dx, Mp, (const float *)db, dout, nullptr, ablate,
-                                 tile_n ? tile_n : 256);
-        else {
-            g_force_bn = tile_n;
-            g_gemm_variant = ablate == -2 ? 1 : ablate == -4 ? 2 : 0;   // -2: gemmq (2 x 4), -4: gemmqw
-            launch_gemm(W, (const uint16_t *)dx, Mp, (const float *)db, epi, (const float *)dr, dout, nullptr);
-            g_force_bn = 0;
-            g_gemm_variant = 0;
-        }
+        g_force_bn = tile_n;
+        g_gemm_variant = ablate == -2 ? 2 : 0;   // -2: gemmqw everywhere
+        launch_gemm(W, (const uint16_t *)dx, Mp, (const float *)db, epi, (const float *)dr, dout, nullptr);
+        g_force_bn = 0;
+        g_gemm_variant = 0;
     };
     if (ablate <= -3 && ablate >= -40 && fdev == FMT_Q4_0) {
         // -3: stamps; -3 - d: stamps + ablation d of gemmqw (kernels.h)

@@ -1,364 +1,655 @@
-// f16-weight GEMM for gfx950:  Y[m][n] = epi( sum_k X[m][k] * W[n][k] )
-//   X  f16 [M][K] activations (tokens x features), M a multiple of 256
-//   W  f16 [N][K] weights (f16 files; f32 files converted at load) in the
-//      K-step-major layout of kernels.h.  Quantized weights: gemm_q.hip.
+// Linear layers for gfx950:  Y[m][n] = epi( sum_k X[m][k] * W[n][k] ),
+// X f16 [M][K] (tokens x features), W in f16 / q4_0 / q4_1 / q8_0 in the
+// "register" layout of kernels.h.  MFMA v_mfma_f32_32x32x16_f16 with A = W rows
+// (32 features) and B = X rows (32 tokens), so an accumulator lane is a token
+// and its registers hold runs of 4 consecutive features.
 //
-// Workgroup = 8 waves (4 along tokens x 2 along features), tile 256 tokens x BN
-// features x 64 k per step, BN = 256 for the wide projections (QKV, FFN-up)
-// and 128 for the N = n_embd ones.  The bytes a CU must pull per FLOP set the
-// speed here (the L2 -> LDS fill rate, not the MFMA): a 256 x 256 step moves
-// 32 KiB of X + 8 KiB of q4 weights for 8.4 MFLOP.
-//   * X arrives by LDS-DMA (global_load_lds_dwordx4) into a ring of stages with
-//     an XOR swizzle applied to the per-lane SOURCE address (the LDS image stays
-//     lane-linear, as LDS-DMA requires).
-//   * W: f16 tiles arrive the same way; q-format tiles arrive raw (nibbles /
-//     int8 + the row's f16 scale dword, per lane) by LDS-DMA into a staging
-//     area, and the lane that loaded a block expands it to f16 into the
-//     swizzled W stage (its own vmcnt orders that read; no other lane needs it).
-//   * Every global load of the K loop is LDS-DMA; the loop waits with a full
-//     vmcnt(0) only where that is the exact wait, so no prefetch is drained
-//     early, and barriers are raw s_barrier (a __syncthreads drains vmcnt).
-//   * MFMA v_mfma_f32_32x32x16_f16; A = W rows, B = X rows, so the accumulator
-//     lane is a token and its registers hold runs of 4 consecutive features.
-//   * Epilogue through LDS: bias / GELU applied in registers and the tile
-//     staged (f16, or f32 for the residual form), then written as whole rows,
-//     16 B per lane.
-//   * Tiles are remapped so blocks that share an XCD (b, b+8, ...) walk
-//     consecutive tiles of the same X rows: the X panel stays in that XCD's L2.
+// Weights never touch LDS.  Each lane loads exactly the bytes of its own A
+// fragments (one 16-B load per K-step for q4, two for q8, four for f16 -- the
+// repack makes them contiguous) into a 3-set register ring two K-steps ahead,
+// and expands quantized words to f16 in registers (nibble | 0x6400 magic, one
+// packed subtract and one packed multiply by the block scale) between MFMAs.
+// LDS carries only the activations, by LDS-DMA (global_load_lds_dwordx4) with
+// an XOR swizzle applied to the per-lane SOURCE address, so ds_read_b128 of a
+// B fragment is conflict-light.
+//
+// Two kernels (both: waves along the FEATURES, so every A fragment feeds
+// 256/32 or 128/32 MFMAs and each weight byte is loaded by one wave):
+//   gemmqw: one 8-wave workgroup per CU, tile 256 tokens x 256 features
+//           (or 2 x 4 waves, 256 x 128), 3-stage X ring.
+//   gemmqv: two 4-wave workgroups per CU, tile BM (256 / 128) tokens x 128
+//           features, 2-stage X ring -- the co-resident workgroups drift apart
+//           so one's epilogue overlaps the other's MFMAs.
+// Waits: every K-step issues its loads, then an explicit `s_waitcnt vmcnt(N)`
+// equal to the operations known to be in flight -- a run-time no-op that tells
+// the compiler's waitcnt pass the current set has landed, so it adds no
+// vmcnt(0) (which would drain the LDS-DMA ring) before the MFMAs.  The K loop
+// runs whole unguarded triples (past the end the issues re-read step KS-1) so
+// that count is the same on every path the compiler sees.
+// Epilogue straight from the accumulators: bias, era GELU or residual add;
+// f16 rows widened to 16-B stores with v_permlane32_swap, f32 rows as 16-B runs.
 #include "device_common.h"
 #include "host_common.h"
 #include "kernels.h"
 
 namespace emb {
 
-int g_force_bn = 0;   // tests: force the tile width (0 = heuristic)
-
 namespace {
 
 constexpr int GM = GEMM_BM;   // 256 tokens per tile
-constexpr int GK = 64;        // k per step (two quant blocks)
+constexpr int GK = 64;
+constexpr int XS = 3;                        // X stages
+constexpr int X_BYTES = GM * GK * 2;          // 32 KiB
 
-template <int BN>
-struct Cfg {
-    static constexpr int XS = BN == 256 ? 2 : 3;             // X stages
-    static constexpr int NI = BN / 64;                      // 32-feature subtiles per wave
-    static constexpr int X_BYTES = GM * GK * 2;              // 32 KiB
-    static constexpr int W_BYTES = BN * GK * 2;              // 16 / 32 KiB
-    static constexpr int OFF_X = 0;
-    static constexpr int OFF_W = OFF_X + XS * X_BYTES;        // 2 stages
-    static constexpr int OFF_RQ = OFF_W + 2 * W_BYTES;        // raw quant payload of one step
-    static constexpr int RQ_BYTES = BN == 256 ? 16384 : 8192;
-    static constexpr int OFF_RS = OFF_RQ + RQ_BYTES;          // raw scale dwords, one per lane
-    static constexpr int OFF_RM = OFF_RS + 2048;              // raw min dwords (q4_1)
-    static constexpr int LDS_BYTES = OFF_RM + 2048;
-};
 
-// Byte offset of 16-byte chunk c (0..7) of row r in a [rows][64 x f16] image.
-// Two 128-B rows share a 256-B bank row; XOR with (r>>1)&7 spreads the 16 rows
-// of a ds_read_b128 lane group over all 16 slots.
-__device__ __forceinline__ int swz(int r, int c) { return (r << 7) | ((c ^ ((r >> 1) & 7)) << 4); }
-
-// X tile: 256 rows x 128 B = 32 LDS-DMA instructions, 4 per wave.
-struct XSrc {
-    const h16 *p[4];
-    __device__ void init(const h16 *X, int K, int m0, int wave, int lane)
-    {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int r = 32 * wave + 8 * i + (lane >> 3);
-            const int c = (lane & 7) ^ ((r >> 1) & 7);
-            p[i] = X + (size_t)(m0 + r) * K + c * 8;
-        }
-    }
-    __device__ void issue(int ks, char *xs, int wave) const
-    {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) glds<16>(p[i] + ks * GK, xs + ((32 * wave + 8 * i) << 7));
-    }
-};
-
-// ---- weight paths: issue() starts the LDS-DMA of step ks, expand() makes the
-// f16 W stage out of the raw bytes this lane loaded ----
-template <int FMT, int BN>
-struct WPath;
-
-template <int BN>
-struct WPath<FMT_F16, BN> {   // f16 (f32 files are converted at load)
-    static constexpr int NL = BN / 64;   // instructions per wave
-    const h16 *p[NL];
-    size_t step;
-    __device__ void init(const DevWeight &W, int n0, int wave, int lane)
-    {
-        step = (size_t)W.N * GK;
-#pragma unroll
-        for (int i = 0; i < NL; ++i) {
-            const int r = (BN / 8) * wave + 8 * i + (lane >> 3);
-            const int c = (lane & 7) ^ ((r >> 1) & 7);
-            p[i] = (const h16 *)W.qs + (size_t)min(n0 + r, W.N - 1) * GK + c * 8;
-        }
-    }
-    __device__ void issue(int ks, char *wst, char *, int wave) const
-    {
-#pragma unroll
-        for (int i = 0; i < NL; ++i) glds<16>(p[i] + ks * step, wst + (((BN / 8) * wave + 8 * i) << 7));
-    }
-    __device__ void expand(char *, const char *, int, int) const {}
-};
-
-// Ablation switches (diagnostic builds only; production instantiates ABL = 0).
-enum : int { ABL_NO_LOADS = 1, ABL_NO_EXPAND = 2, ABL_NO_MFMA = 4, ABL_NO_EPILOGUE = 8 };
-
-template <int FMT, int EPI, int BN, int ABL = 0>
-__global__ __launch_bounds__(512, 1) void gemm_kernel(DevWeight W, const h16 *__restrict__ X,
-                                                      const float *__restrict__ bias, const float *__restrict__ res,
-                                                      void *__restrict__ out, int nN, int nTiles)
+// Weight words are ordinary (compiler-visible) loads: the compiler must own the
+// registers of an in-flight load (an asm load's destination can be reused by
+// the register allocator before the data arrives).  They are issued before the
+// step's LDS-DMA, so the compiler's wait at their first use (next step) only
+// retires X(ks+2), which has had a whole step of MFMAs to land.
+__device__ __forceinline__ uint4 gload16(const void *p) { return *(const uint4 *)p; }
+__device__ __forceinline__ uint32_t gload4(const void *p) { return *(const uint32_t *)p; }
+// pin: an empty volatile asm that "rewrites" the registers, so their uses
+// cannot be scheduled above the (side-effecting) explicit wait before it.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void pin(uint4 &q)
 {
-    using C = Cfg<BN>;
-    constexpr int NI = C::NI;
-    __shared__ __attribute__((aligned(16))) char smem[C::LDS_BYTES];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    // XCD-aware bijective remap: blocks b, b+8, ... (one XCD) get consecutive tiles
-    const int b = blockIdx.x, xcd = b & 7, q = nTiles >> 3, rr = nTiles & 7;
-    const int t = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (b >> 3);
-    const int m0 = (t / nN) * GM, n0 = (t % nN) * BN;
-    const int K = W.K, N = W.N, KS = K / GK;
-    const int wm = wave & 3, wn = wave >> 2, lr = lane & 31, hi = lane >> 5;
-
-    XSrc xsrc;
-    xsrc.init(X, K, m0, wave, lane);
-    WPath<FMT, BN> wp;
-    wp.init(W, n0, wave, lane);
-
-    f32x16 acc[NI][2];
-#pragma unroll
-    for (int i = 0; i < NI; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-    // prologue: W(0) and X(0) landed (+ X(1) in flight with 3 stages)
-    wp.issue(0, smem + C::OFF_W, smem, wave);
-    xsrc.issue(0, smem + C::OFF_X, wave);
-    wait_vmcnt<0>();
-    wp.expand(smem + C::OFF_W, smem, wave, lane);
-    if (C::XS == 3 && KS > 1) xsrc.issue(1, smem + C::OFF_X + C::X_BYTES, wave);
-    lds_barrier();
-
-    // Step ks (2 X stages): issue W(ks+1), X(ks+1) -> MFMAs on step ks -> vmcnt(0)
-    //   -> expand W(ks+1) -> barrier.
-    // Step ks (3 X stages): issue W(ks+1) -> MFMAs -> vmcnt(0) -> expand W(ks+1)
-    //   -> issue X(ks+2) -> barrier.
-    // Either way vmcnt(0) is the exact wait (the loads it waits for are needed
-    // next), so the compiler's own conservative waits drain nothing early.
-    const int sw = (lr >> 1) & 7;   // swizzle key of every row this lane reads
-    int ra[NI];
-#pragma unroll
-    for (int i = 0; i < NI; ++i) ra[i] = (wn * (BN / 2) + 32 * i + lr) << 7;
-    const int rb0 = (wm * 64 + lr) << 7, rb1 = (wm * 64 + 32 + lr) << 7;
-    int xs_cur = 0;
-    for (int ks = 0; ks < KS; ++ks) {
-        const bool more = ks + 1 < KS;
-        const int xs_nxt = xs_cur + 1 == C::XS ? 0 : xs_cur + 1;
-        const int xs_nn = xs_nxt + 1 == C::XS ? 0 : xs_nxt + 1;
-        if (more && !(ABL & ABL_NO_LOADS)) {
-            wp.issue(ks + 1, smem + C::OFF_W + ((ks + 1) & 1) * C::W_BYTES, smem, wave);
-            if (C::XS == 2) xsrc.issue(ks + 1, smem + C::OFF_X + xs_nxt * C::X_BYTES, wave);
-        }
-        const char *xs = smem + C::OFF_X + xs_cur * C::X_BYTES;
-        const char *ws = smem + C::OFF_W + (ks & 1) * C::W_BYTES;
-        h16x8 a[NI], b0, b1;
-        {
-            const int cx = (hi ^ sw) << 4;
-#pragma unroll
-            for (int i = 0; i < NI; ++i) a[i] = *(const h16x8 *)(ws + ra[i] + cx);
-            b0 = *(const h16x8 *)(xs + rb0 + cx);
-            b1 = *(const h16x8 *)(xs + rb1 + cx);
-        }
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-            h16x8 na[NI], nb0, nb1;
-            if (kk < 3) {   // next fragments in flight under this k-slice's MFMAs
-                const int cx = ((2 * kk + 2 + hi) ^ sw) << 4;
-#pragma unroll
-                for (int i = 0; i < NI; ++i) na[i] = *(const h16x8 *)(ws + ra[i] + cx);
-                nb0 = *(const h16x8 *)(xs + rb0 + cx);
-                nb1 = *(const h16x8 *)(xs + rb1 + cx);
-            }
-            if constexpr (!(ABL & ABL_NO_MFMA)) {
-                __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-                for (int i = 0; i < NI; ++i) {
-                    acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b0, acc[i][0], 0, 0, 0);
-                    acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b1, acc[i][1], 0, 0, 0);
-                }
-                __builtin_amdgcn_s_setprio(0);
-            } else {
-#pragma unroll
-                for (int i = 0; i < NI; ++i) asm volatile("" ::"v"(a[i]), "v"(b0), "v"(b1));
-            }
-            if (kk < 3) {
-#pragma unroll
-                for (int i = 0; i < NI; ++i) a[i] = na[i];
-                b0 = nb0;
-                b1 = nb1;
-            }
-        }
-        if (more) {
-            wait_vmcnt<0>();
-            if constexpr (!(ABL & ABL_NO_EXPAND)) wp.expand(smem + C::OFF_W + ((ks + 1) & 1) * C::W_BYTES, smem, wave, lane);
-            if (C::XS == 3 && ks + 2 < KS && !(ABL & ABL_NO_LOADS))
-                xsrc.issue(ks + 2, smem + C::OFF_X + xs_nn * C::X_BYTES, wave);
-            lds_barrier();
-        }
-        xs_cur = xs_nxt;
-    }
-
-    // ---- epilogue ----
-    if constexpr ((ABL & ABL_NO_EPILOGUE) != 0) {   // keep the accumulators alive, store one word per lane
-        float s = 0.f;
-#pragma unroll
-        for (int i = 0; i < NI; ++i)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) s += acc[i][0][r] + acc[i][1][r];
-        ((float *)out)[(size_t)blockIdx.x * 512 + tid] = s;
-        return;
-    }
-    lds_barrier();   // every wave is done with the operand stages
-    if constexpr (EPI == EPI_BIAS_RES_F32) {
-        // f32 staging: 256 rows x (BN*4 + 16) B, then res + (bias + acc) per 16-B chunk
-        constexpr int ES = BN * 4 + 16;
-        static_assert(GM * ES <= C::LDS_BYTES, "f32 staging must fit");
-#pragma unroll
-        for (int i = 0; i < NI; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int m = wm * 64 + j * 32 + lr;
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const int n = wn * (BN / 2) + i * 32 + 8 * g + 4 * hi;
-                    f32x4 v = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
-                    *(f32x4 *)(smem + m * ES + n * 4) = v;
-                }
-            }
-        lds_barrier();
-        constexpr int CPR = BN / 4;              // 16-B chunks per row
-        constexpr int RPI = 512 / CPR;           // rows per pass
-        const int nl = (tid % CPR) * 4, gn = n0 + nl;
-        if (gn >= N) return;
-        const f32x4 bb = *(const f32x4 *)(bias + gn);
-#pragma unroll 4
-        for (int it = 0; it < GM / RPI; ++it) {
-            const int m = it * RPI + tid / CPR;
-            const size_t gm = (size_t)(m0 + m);
-            const f32x4 v = *(const f32x4 *)(smem + m * ES + nl * 4);
-            const f32x4 r = *(const f32x4 *)(res + gm * N + gn);
-            f32x4 o;
-            o[0] = r[0] + (bb[0] + v[0]); o[1] = r[1] + (bb[1] + v[1]);
-            o[2] = r[2] + (bb[2] + v[2]); o[3] = r[3] + (bb[3] + v[3]);
-            *(f32x4 *)((float *)out + gm * N + gn) = o;
-        }
-    } else {
-        // bias (+ GELU) in registers, f16 staging: 256 rows x (BN*2 + 16) B
-        constexpr int ES = BN * 2 + 16;
-        static_assert(GM * ES <= C::LDS_BYTES, "f16 staging must fit");
-#pragma unroll
-        for (int i = 0; i < NI; ++i)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int n = wn * (BN / 2) + i * 32 + 8 * g + 4 * hi;
-                const f32x4 bb = *(const f32x4 *)(bias + min(n0 + n, N - 4));
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const int m = wm * 64 + j * 32 + lr;
-                    h16x4 o;
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const float v = bb[e] + acc[i][j][4 * g + e];
-                        o[e] = EPI == EPI_BIAS_GELU_F16 ? gelu_era(v) : (h16)v;
-                    }
-                    *(h16x4 *)(smem + m * ES + n * 2) = o;
-                }
-            }
-        lds_barrier();
-        constexpr int CPR = BN / 8;              // 16-B chunks (8 x f16) per row
-        constexpr int RPI = 512 / CPR;
-        const int nl = (tid % CPR) * 8, gn = n0 + nl;
-        if (gn >= N) return;
-#pragma unroll 4
-        for (int it = 0; it < GM / RPI; ++it) {
-            const int m = it * RPI + tid / CPR;
-            *(uint4 *)((h16 *)out + (size_t)(m0 + m) * N + gn) = *(const uint4 *)(smem + m * ES + nl * 2);
-        }
-    }
+    u32x4 v = __builtin_bit_cast(u32x4, q);
+    asm volatile("" : "+v"(v));
+    q = __builtin_bit_cast(uint4, v);
 }
-
-template <int FMT, int BN>
-void dispatch_bn(const DevWeight &W, const h16 *x, int M, const float *bias, int epi, const float *res, void *out,
-                 hipStream_t s)
-{
-    const int nN = (W.N + BN - 1) / BN, nTiles = (M / GM) * nN;
-    if (epi == EPI_BIAS_F16)
-        gemm_kernel<FMT, EPI_BIAS_F16, BN><<<nTiles, 512, 0, s>>>(W, x, bias, res, out, nN, nTiles);
-    else if (epi == EPI_BIAS_GELU_F16)
-        gemm_kernel<FMT, EPI_BIAS_GELU_F16, BN><<<nTiles, 512, 0, s>>>(W, x, bias, res, out, nN, nTiles);
-    else if constexpr (BN == 128)   // the f32 residual tile only fits 128 wide
-        gemm_kernel<FMT, EPI_BIAS_RES_F32, BN><<<nTiles, 512, 0, s>>>(W, x, bias, res, out, nN, nTiles);
-}
+__device__ __forceinline__ void pin(uint32_t &v) { asm volatile("" : "+v"(v)); }
 
 template <int FMT>
-void dispatch(const DevWeight &W, const uint16_t *X, int M, const float *bias, int epi, const float *res, void *out,
-              hipStream_t s)
+struct QRegs;   // one K-step of this lane's weight words for one 32-feature subtile
+
+template <int FMT>
+struct QRegsQ4 {
+    uint4 q;           // words kk = 0..3 of lane half h
+    uint32_t d, m;     // scale (and min) dword: (block 0, block 1)
+    static constexpr int LOADS = FMT == FMT_Q4_1 ? 3 : 2;
+    __device__ void load(const uint8_t *pq, const uint32_t *pd, const uint32_t *pm)
+    {
+        q = gload16(pq);
+        d = gload4(pd);
+        if (FMT == FMT_Q4_1) m = gload4(pm);
+    }
+    __device__ void pin_all() { pin(q); pin(d); if (FMT == FMT_Q4_1) pin(m); }
+    // A fragment of k-slice kk: 8 f16 = (q - 8) d  |  q d + m
+    __device__ h16x8 frag(int kk) const
+    {
+        const uint32_t w = kk == 0 ? q.x : kk == 1 ? q.y : kk == 2 ? q.z : q.w;
+        const uint16_t dh = kk < 2 ? (uint16_t)(d & 0xffffu) : (uint16_t)(d >> 16);
+        const h16x2 d2 = {as_h(dh), as_h(dh)};
+        h16x2 m2 = {(h16)0.0f, (h16)0.0f};
+        if (FMT == FMT_Q4_1) {
+            const uint16_t mh = kk < 2 ? (uint16_t)(m & 0xffffu) : (uint16_t)(m >> 16);
+            m2 = h16x2{as_h(mh), as_h(mh)};
+        }
+        const h16 o = FMT == FMT_Q4_1 ? (h16)-1024.0f : (h16)-1032.0f;
+        const h16x2 off = {o, o};
+        h16x8 a;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            h16x2 hh = as_h2(((w >> (4 * p)) & 0x000F000Fu) | 0x64006400u) + off;
+            hh = FMT == FMT_Q4_1 ? hh * d2 + m2 : hh * d2;
+            a[2 * p] = hh[0];
+            a[2 * p + 1] = hh[1];
+        }
+        return a;
+    }
+};
+template <> struct QRegs<FMT_Q4_0> : QRegsQ4<FMT_Q4_0> {};
+template <> struct QRegs<FMT_Q4_1> : QRegsQ4<FMT_Q4_1> {};
+
+template <>
+struct QRegs<FMT_Q8_0> {
+    uint4 q0, q1;      // 8 bytes per k-slice: kk 0,1 in q0, kk 2,3 in q1
+    uint32_t d;
+    static constexpr int LOADS = 3;
+    __device__ void load(const uint8_t *pq, const uint32_t *pd, const uint32_t *)
+    {
+        q0 = gload16(pq);
+        q1 = gload16(pq + 16);
+        d = gload4(pd);
+    }
+    __device__ void pin_all() { pin(q0); pin(q1); pin(d); }
+    __device__ h16x8 frag(int kk) const
+    {
+        const uint32_t w0 = kk == 0 ? q0.x : kk == 1 ? q0.z : kk == 2 ? q1.x : q1.z;
+        const uint32_t w1 = kk == 0 ? q0.y : kk == 1 ? q0.w : kk == 2 ? q1.y : q1.w;
+        const uint16_t dh = kk < 2 ? (uint16_t)(d & 0xffffu) : (uint16_t)(d >> 16);
+        const h16x2 d2 = {as_h(dh), as_h(dh)};
+        const h16x2 off = {(h16)-1152.0f, (h16)-1152.0f};   // bytes (q ^ 0x80), order e0 e2 e1 e3
+        h16x8 a;
+        const h16x2 p0 = (as_h2((w0 & 0x00FF00FFu) | 0x64006400u) + off) * d2;
+        const h16x2 p1 = (as_h2(((w0 >> 8) & 0x00FF00FFu) | 0x64006400u) + off) * d2;
+        const h16x2 p2 = (as_h2((w1 & 0x00FF00FFu) | 0x64006400u) + off) * d2;
+        const h16x2 p3 = (as_h2(((w1 >> 8) & 0x00FF00FFu) | 0x64006400u) + off) * d2;
+        a[0] = p0[0]; a[1] = p0[1]; a[2] = p1[0]; a[3] = p1[1];
+        a[4] = p2[0]; a[5] = p2[1]; a[6] = p3[0]; a[7] = p3[1];
+        return a;
+    }
+};
+
+template <>
+struct QRegs<FMT_F16> {        // f16 weights (f32 files are converted at load): no expansion
+    uint4 q[4];                // k-slices kk = 0..3 of lane half h: 8 f16 each
+    static constexpr int LOADS = 4;
+    __device__ void load(const uint8_t *pq, const uint32_t *, const uint32_t *)
+    {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) q[i] = gload16(pq + 16 * i);
+    }
+    __device__ void pin_all()
+    {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pin(q[i]);
+    }
+    __device__ h16x8 frag(int kk) const { return __builtin_bit_cast(h16x8, q[kk]); }
+};
+
+// weight bytes per (K-step, feature) record
+template <int FMT>
+constexpr int qrec_bytes() { return FMT == FMT_F16 ? 128 : FMT == FMT_Q8_0 ? 64 : 32; }
+
+// ---------------------------------------------------------------------------
+// gemmqw: the same contraction with the 8 waves laid out along the FEATURES.
+// Tile 256 tokens x BN features, BN = 32 * 8 / WM; wave w owns features
+// n0 + 32*(w % (8/WM)) .. +31 and tokens (w / (8/WM)) * 256/WM .. +256/WM-1.
+// Every A fragment (dequantized weights) therefore feeds 256/WM/32 MFMAs
+// (8 at WM = 1: half the dequant VALU per MFMA of the 2 x 4 layout) and each
+// weight byte is loaded by exactly one wave.  Weights: a 3-set register ring,
+// two K-steps ahead; X: 3-stage LDS-DMA ring, two K-steps ahead; one barrier
+// per K-step.  Epilogue straight from the accumulators (no LDS staging):
+// f16 rows widened to 16-B stores with v_permlane32_swap, f32 rows as 16-B
+// runs of 4 features.
+// ---------------------------------------------------------------------------
+// DIAG (diagnostics builds only): 0x10 stamps; ablations 0x1 no dequant (raw
+// words as A), 0x2 no B ds_reads (fragments from the prologue), 0x4 no barrier
+// in the K loop, 0x8 no MFMA.
+template <int FMT, int EPI, int WM, int DIAG = 0>
+__global__ __launch_bounds__(512, 1) void gemmqw_kernel(DevWeight W, const h16 *__restrict__ X,
+                                                        const float *__restrict__ bias, const float *__restrict__ res,
+                                                        void *__restrict__ out, int nN, int nTiles,
+                                                        uint64_t *__restrict__ stamps = nullptr)
 {
-    const h16 *x = (const h16 *)X;
-    // 256-wide tiles halve the bytes per FLOP; use them when they still fill
-    // the chip (>= 2 rounds of 256 CUs) and the residual (f32) epilogue is not needed.
-    const bool wide = g_force_bn ? (g_force_bn == 256 && epi != EPI_BIAS_RES_F32 && W.N % 256 == 0)
-                                 : (epi != EPI_BIAS_RES_F32 && W.N % 256 == 0 && (long)(M / GM) * (W.N / 256) >= 512);
-    if (wide) dispatch_bn<FMT, 256>(W, x, M, bias, epi, res, out, s);
-    else dispatch_bn<FMT, 128>(W, x, M, bias, epi, res, out, s);
+    // STAMP (diagnostics build only): s_memtime at start / after the prologue /
+    // after the K loop / after the epilogue, per wave, into stamps[]
+    constexpr bool STAMP = (DIAG & 0x10) != 0;
+    uint64_t ts[4];
+    if constexpr (STAMP) ts[0] = __builtin_amdgcn_s_memtime();
+    constexpr int WN = 8 / WM;                 // waves along the features
+    constexpr int BN = 32 * WN;                // 256 (WM 1) or 128 (WM 2)
+    constexpr int TM = GM / WM;                // tokens per wave
+    constexpr int NJ = TM / 32;                // B fragments (32-token groups) per k-slice
+    constexpr int QB = qrec_bytes<FMT>();
+    constexpr int P = QRegs<FMT>::LOADS + 4;   // vector-memory ops issued per K-step per wave
+    __shared__ __attribute__((aligned(16))) char smem[XS * X_BYTES];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int b = blockIdx.x, xcd = b & 7, qq = nTiles >> 3, rr = nTiles & 7;
+    const int t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
+    const int m0 = (t / nN) * GM, n0 = (t % nN) * BN;
+    const int K = W.K, N = W.N, KS = K / GK;
+    const int wm = wave / WN, wn = wave % WN, lr = lane & 31, hi = lane >> 5;
+    const int nw = n0 + 32 * wn;               // this wave's first feature
+
+    const h16 *xp[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = 32 * wave + 8 * i + (lane >> 3);
+        xp[i] = X + (size_t)(m0 + r) * K + (((lane & 7) ^ ((r >> 1) & 7)) * 8);
+    }
+#define EMB_ISSUE_XW(ks_, stage_)                                                                   \
+    {                                                                                               \
+        char *dst_ = smem + (stage_) * X_BYTES + ((32 * wave) << 7);                                \
+        glds<16>(xp[0] + (ks_) * GK, dst_);                                                         \
+        glds<16>(xp[1] + (ks_) * GK, dst_ + (8 << 7));                                              \
+        glds<16>(xp[2] + (ks_) * GK, dst_ + (16 << 7));                                             \
+        glds<16>(xp[3] + (ks_) * GK, dst_ + (24 << 7));                                             \
+    }
+    const int nrow = min(nw + lr, N - 1);
+    const uint8_t *wq = (const uint8_t *)W.qs + (size_t)nrow * QB + (QB / 2) * hi;
+    const uint32_t *wd = (const uint32_t *)W.d + nrow;
+    const uint32_t *wmn = FMT == FMT_Q4_1 ? (const uint32_t *)W.m + nrow : nullptr;
+    const size_t qstep = (size_t)N * QB, sstep = (size_t)N;
+
+    f32x16 acc[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+
+    // prologue: W(0), X(0), W(1), X(1) in flight; retire W(0), X(0)
+    QRegs<FMT> w0, w1, w2;
+    const int k1 = min(1, KS - 1);
+    w0.load(wq, wd, wmn);
+    EMB_ISSUE_XW(0, 0)
+    w1.load(wq + k1 * qstep, wd + k1 * sstep, FMT == FMT_Q4_1 ? wmn + k1 * sstep : nullptr);
+    EMB_ISSUE_XW(k1, 1)
+    wait_vmcnt<P>();
+    lds_barrier();
+    if constexpr (STAMP) ts[1] = __builtin_amdgcn_s_memtime();
+
+    const int sw = (lr >> 1) & 7;
+    const int rbase = (wm * TM + lr) << 7;
+    int st = 0;
+    h16x8 bdiag[(DIAG & 0x2) ? NJ : 1];
+    if constexpr (DIAG & 0x2) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) bdiag[j] = *(const h16x8 *)(smem + rbase + (j << 12) + (hi << 4));
+    }
+
+// One K-step with CUR's weights: W(ks+2) -> NXT2, X(ks+2) -> its stage (clamped:
+// past the end the issues re-read step KS-1), explicit no-op wait declaring CUR
+// landed, MFMAs, then retire step ks+1's operands and barrier.
+#define EMB_WSTEP(CUR, NXT2, ks_)                                                                         \
+    {                                                                                                     \
+        const int ksx = (ks_);                                                                            \
+        const int st2 = st == 0 ? 2 : st - 1;                                                             \
+        {                                                                                                 \
+            const int k2 = min(ksx + 2, KS - 1);                                                          \
+            NXT2.load(wq + k2 * qstep, wd + k2 * sstep, FMT == FMT_Q4_1 ? wmn + k2 * sstep : nullptr);    \
+            EMB_ISSUE_XW(k2, st2)                                                                         \
+            wait_vmcnt<2 * P>();                                                                          \
+            CUR.pin_all();                                                                                \
+        }                                                                                                 \
+        const char *xs = smem + st * X_BYTES + rbase;                                                     \
+        if constexpr (DIAG & 0x20) {                                                                      \
+            /* software-pipelined: B fragments and A dequant of k-slice kk+1 issued */                   \
+            /* between the MFMAs of kk (sched_group_barrier pins the interleave) */                       \
+            h16x8 bc[NJ], bnx[NJ];                                                                        \
+            _Pragma("unroll") for (int j = 0; j < NJ; ++j) bc[j] = *(const h16x8 *)(xs + (j << 12) + ((hi ^ sw) << 4)); \
+            h16x8 ac = CUR.frag(0), anx;                                                                  \
+            _Pragma("unroll") for (int kk = 0; kk < 4; ++kk)                                              \
+            {                                                                                             \
+                if (kk < 3) {                                                                             \
+                    const int cx = ((2 * kk + 2 + hi) ^ sw) << 4;                                         \
+                    _Pragma("unroll") for (int j = 0; j < NJ; ++j) bnx[j] = *(const h16x8 *)(xs + (j << 12) + cx); \
+                    anx = CUR.frag(kk + 1);                                                               \
+                }                                                                                         \
+                _Pragma("unroll") for (int j = 0; j < NJ; ++j) acc[j] =                                   \
+                    __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bc[j], acc[j], 0, 0, 0);                   \
+                if (kk < 3) {                                                                             \
+                    _Pragma("unroll") for (int j = 0; j < NJ; ++j) {                                      \
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                \
+                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                \
+                        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);                                \
+                    }                                                                                     \
+                    _Pragma("unroll") for (int j = 0; j < NJ; ++j) bc[j] = bnx[j];                        \
+                    ac = anx;                                                                             \
+                }                                                                                         \
+            }                                                                                             \
+        } else                                                                                            \
+        _Pragma("unroll") for (int kk = 0; kk < 4; ++kk)                                                  \
+        {                                                                                                 \
+            const int cx = ((2 * kk + hi) ^ sw) << 4;                                                     \
+            h16x8 bf[NJ];                                                                                 \
+            if constexpr (DIAG & 0x2) {                                                                   \
+                _Pragma("unroll") for (int j = 0; j < NJ; ++j) bf[j] = bdiag[j];                          \
+            } else {                                                                                      \
+                _Pragma("unroll") for (int j = 0; j < NJ; ++j) bf[j] = *(const h16x8 *)(xs + (j << 12) + cx); \
+            }                                                                                             \
+            h16x8 a;                                                                                      \
+            if constexpr ((DIAG & 0x1) && FMT != FMT_F16) a = __builtin_bit_cast(h16x8, CUR.q);                               \
+            else a = CUR.frag(kk);                                                                        \
+            if constexpr (DIAG & 0x8) {                                                                   \
+                _Pragma("unroll") for (int j = 0; j < NJ; ++j) asm volatile("" :: "v"(a), "v"(bf[j]));   \
+            } else {                                                                                      \
+                _Pragma("unroll") for (int j = 0; j < NJ; ++j) acc[j] =                                   \
+                    __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bf[j], acc[j], 0, 0, 0);                    \
+            }                                                                                             \
+        }                                                                                                 \
+        wait_vmcnt<P>(); /* step ks+1's W and X landed; step ks+2's may fly */                           \
+        if constexpr (DIAG & 0x4) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                     \
+        else lds_barrier();                                                                               \
+        st = st == 2 ? 0 : st + 1;                                                                        \
+    }
+
+    // whole triples in the loop (no guarded steps: a guard is a path on which
+    // the compiler's waitcnt model loses track and drains with vmcnt(0)), then
+    // the 0-2 remaining steps
+    int ks = 0;
+    for (; ks + 3 <= KS; ks += 3) {
+        EMB_WSTEP(w0, w2, ks)
+        EMB_WSTEP(w1, w0, ks + 1)
+        EMB_WSTEP(w2, w1, ks + 2)
+    }
+    if (ks < KS) {
+        EMB_WSTEP(w0, w2, ks)
+        if (ks + 1 < KS) EMB_WSTEP(w1, w0, ks + 1)
+    }
+#undef EMB_WSTEP
+#undef EMB_ISSUE_XW
+    wait_vmcnt<0>();   // the clamped tail re-reads still write LDS / registers
+    if constexpr (STAMP) ts[2] = __builtin_amdgcn_s_memtime();
+
+    // ---- epilogue: lane holds token 32j + lr, features nw + 8g + 4hi + e ----
+    if (nw >= N) return;                       // wave-uniform (N % 32 == 0)
+    const int mrow = m0 + wm * TM + lr;
+    f32x4 bb[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) bb[g] = *(const f32x4 *)(bias + nw + 8 * g + 4 * hi);
+    if constexpr (EPI == EPI_BIAS_RES_F32) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const size_t rowo = (size_t)(mrow + 32 * j) * N + nw + 4 * hi;
+            f32x4 rv[4];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) rv[g] = *(const f32x4 *)(res + rowo + 8 * g);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                f32x4 o;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[e] = rv[g][e] + (bb[g][e] + acc[j][4 * g + e]);
+                *(f32x4 *)((float *)out + rowo + 8 * g) = o;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            uint32_t pk[4][2];                 // group g: 4 f16 of features 8g + 4hi + 0..3
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                h16 o[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float v = bb[g][e] + acc[j][4 * g + e];
+                    o[e] = EPI == EPI_BIAS_GELU_F16 ? gelu_era(v) : (h16)v;
+                }
+                pk[g][0] = __builtin_bit_cast(uint32_t, h16x2{o[0], o[1]});
+                pk[g][1] = __builtin_bit_cast(uint32_t, h16x2{o[2], o[3]});
+            }
+            // T21: half-exchange pairs (g, g+1) -> lanes 0-31 hold features 8g..8g+7,
+            // lanes 32-63 hold 8g+8..8g+15 of the same token
+            h16 *orow = (h16 *)out + (size_t)(mrow + 32 * j) * N + nw + 8 * hi;
+#pragma unroll
+            for (int g = 0; g < 4; g += 2) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const auto r2 = __builtin_amdgcn_permlane32_swap(pk[g][h], pk[g + 1][h], false, false);
+                    pk[g][h] = r2[0];
+                    pk[g + 1][h] = r2[1];
+                }
+                uint4 v;
+                v.x = pk[g][0]; v.y = pk[g][1]; v.z = pk[g + 1][0]; v.w = pk[g + 1][1];
+                *(uint4 *)(orow + 8 * g) = v;
+            }
+        }
+    }
+    if constexpr (STAMP) {
+        ts[3] = __builtin_amdgcn_s_memtime();
+        if (lane == 0)
+            for (int i = 0; i < 4; ++i) stamps[((size_t)blockIdx.x * 8 + wave) * 4 + i] = ts[i];
+    }
+}
+
+template <int FMT, int WM, int STAMP = 0>
+void dispatch_qw(const DevWeight &W, const h16 *x, int M, const float *bias, int epi, const float *res, void *out,
+                 hipStream_t s, uint64_t *stamps = nullptr)
+{
+    constexpr int BN = 256 / WM;
+    const int nN = (W.N + BN - 1) / BN, nTiles = (M / GM) * nN;
+    if (epi == EPI_BIAS_F16)
+        gemmqw_kernel<FMT, EPI_BIAS_F16, WM, STAMP><<<nTiles, 512, 0, s>>>(W, x, bias, res, out, nN, nTiles, stamps);
+    else if (epi == EPI_BIAS_GELU_F16)
+        gemmqw_kernel<FMT, EPI_BIAS_GELU_F16, WM, STAMP><<<nTiles, 512, 0, s>>>(W, x, bias, res, out, nN, nTiles,
+                                                                              stamps);
+    else
+        gemmqw_kernel<FMT, EPI_BIAS_RES_F32, WM, STAMP><<<nTiles, 512, 0, s>>>(W, x, bias, res, out, nN, nTiles,
+                                                                             stamps);
+}
+
+// ---------------------------------------------------------------------------
+// gemmqv: TWO workgroups per CU.  4 waves (256 threads) per workgroup, tile
+// BM tokens x 128 features, wave w owns features n0 + 32w .. +31 and all BM
+// tokens (NJ = BM/32 B fragments per k-slice).  Two independent workgroups per
+// CU drift apart, so one's epilogue (HBM store burst, GELU VALU) and prologue
+// overlap the other's MFMA loop -- with one workgroup per CU every CU hit its
+// epilogue at the same moment (measured: 30-40 % of the tile time).
+// X: 2-stage LDS-DMA ring (64 KiB at BM 256), one K-step ahead; W: 3-set
+// register ring, two K-steps ahead; one barrier per K-step.
+// ---------------------------------------------------------------------------
+template <int FMT, int EPI, int BM>
+__global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemmqv_kernel(DevWeight W, const h16 *__restrict__ X,
+                                                        const float *__restrict__ bias, const float *__restrict__ res,
+                                                        void *__restrict__ out, int nN, int nTiles)
+{
+    constexpr int BN = 128;
+    constexpr int NJ = BM / 32;
+    constexpr int XB = BM * GK * 2;            // bytes per X stage
+    constexpr int XG = XB / (256 * 16);        // LDS-DMA instructions per wave per stage
+    constexpr int QB = qrec_bytes<FMT>();
+    constexpr int LQ = QRegs<FMT>::LOADS;
+    __shared__ __attribute__((aligned(16))) char smem[2 * XB];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int b = blockIdx.x, xcd = b & 7, qq = nTiles >> 3, rr = nTiles & 7;
+    const int t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
+    const int m0 = (t / nN) * BM, n0 = (t % nN) * BN;
+    const int K = W.K, N = W.N, KS = K / GK;
+    const int lr = lane & 31, hi = lane >> 5;
+    const int nw = n0 + 32 * wave;
+
+    // X LDS-DMA sources: XG instructions per wave, rows (XG*8)*wave + 8i + lane/8
+    const h16 *xp[XG];
+#pragma unroll
+    for (int i = 0; i < XG; ++i) {
+        const int r = 8 * XG * wave + 8 * i + (lane >> 3);
+        xp[i] = X + (size_t)(m0 + r) * K + (((lane & 7) ^ ((r >> 1) & 7)) * 8);
+    }
+#define EMB_ISSUE_XV(ks_, stage_)                                                                   \
+    {                                                                                               \
+        char *dst_ = smem + (stage_) * XB + ((8 * XG * wave) << 7);                                 \
+        _Pragma("unroll") for (int i = 0; i < XG; ++i) glds<16>(xp[i] + (ks_) * GK, dst_ + (i << 10)); \
+    }
+    const int nrow = min(nw + lr, N - 1);
+    const uint8_t *wq = (const uint8_t *)W.qs + (size_t)nrow * QB + (QB / 2) * hi;
+    const uint32_t *wd = (const uint32_t *)W.d + nrow;
+    const uint32_t *wmn = FMT == FMT_Q4_1 ? (const uint32_t *)W.m + nrow : nullptr;
+    const size_t qstep = (size_t)N * QB, sstep = (size_t)N;
+
+    f32x16 acc[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+
+    // prologue: W(0), X(0) -> stage 0, W(1); retire W(0) and X(0)
+    QRegs<FMT> w0, w1, w2;
+    const int k1 = min(1, KS - 1);
+    w0.load(wq, wd, wmn);
+    EMB_ISSUE_XV(0, 0)
+    w1.load(wq + k1 * qstep, wd + k1 * sstep, FMT == FMT_Q4_1 ? wmn + k1 * sstep : nullptr);
+    wait_vmcnt<LQ>();
+    lds_barrier();
+
+    const int sw = (lr >> 1) & 7;
+    const int rbase = lr << 7;
+    int st = 0;
+
+// One K-step with CUR's weights: X(ks+1) -> the other stage, W(ks+2) -> NXT2
+// (clamped past the end), explicit no-op wait declaring CUR landed, MFMAs, then
+// retire X(ks+1) and W(ks+1) (everything but W(ks+2)) and barrier.
+#define EMB_VSTEP(CUR, NXT2, ks_)                                                                         \
+    {                                                                                                     \
+        const int ksx = (ks_);                                                                            \
+        {                                                                                                 \
+            const int kx = min(ksx + 1, KS - 1), k2 = min(ksx + 2, KS - 1);                               \
+            EMB_ISSUE_XV(kx, st ^ 1)                                                                      \
+            asm volatile("" ::: "memory"); /* keep X(ks+1) older than W(ks+2): the end wait splits them */ \
+            NXT2.load(wq + k2 * qstep, wd + k2 * sstep, FMT == FMT_Q4_1 ? wmn + k2 * sstep : nullptr);    \
+            wait_vmcnt<2 * LQ + XG>();                                                                    \
+            CUR.pin_all();                                                                                \
+        }                                                                                                 \
+        const char *xs = smem + st * XB + rbase;                                                          \
+        h16x8 bf[NJ], bn[NJ];                                                                             \
+        _Pragma("unroll") for (int j = 0; j < NJ; ++j) bf[j] = *(const h16x8 *)(xs + (j << 12) + (hi ^ sw) * 16); \
+        _Pragma("unroll") for (int kk = 0; kk < 4; ++kk)                                                  \
+        {                                                                                                 \
+            if (kk < 3) {                                                                                 \
+                const int cx = ((2 * kk + 2 + hi) ^ sw) << 4;                                             \
+                _Pragma("unroll") for (int j = 0; j < NJ; ++j) bn[j] = *(const h16x8 *)(xs + (j << 12) + cx); \
+            }                                                                                             \
+            const h16x8 a = CUR.frag(kk);                                                                 \
+            _Pragma("unroll") for (int j = 0; j < NJ; ++j) acc[j] =                                       \
+                __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bf[j], acc[j], 0, 0, 0);                        \
+            if (kk < 3) {                                                                                 \
+                _Pragma("unroll") for (int j = 0; j < NJ; ++j) bf[j] = bn[j];                             \
+            }                                                                                             \
+        }                                                                                                 \
+        wait_vmcnt<LQ>(); /* X(ks+1), W(ks+1) landed; W(ks+2) may fly */                                 \
+        lds_barrier();                                                                                    \
+        st ^= 1;                                                                                          \
+    }
+
+    int ks = 0;
+    for (; ks + 3 <= KS; ks += 3) {
+        EMB_VSTEP(w0, w2, ks)
+        EMB_VSTEP(w1, w0, ks + 1)
+        EMB_VSTEP(w2, w1, ks + 2)
+    }
+    if (ks < KS) {
+        EMB_VSTEP(w0, w2, ks)
+        if (ks + 1 < KS) EMB_VSTEP(w1, w0, ks + 1)
+    }
+#undef EMB_VSTEP
+#undef EMB_ISSUE_XV
+    wait_vmcnt<0>();
+
+    // ---- epilogue: lane holds token m0 + 32j + lr, features nw + 8g + 4hi + e ----
+    if (nw >= N) return;                       // wave-uniform (N % 32 == 0)
+    const int mrow = m0 + lr;
+    f32x4 bb[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) bb[g] = *(const f32x4 *)(bias + nw + 8 * g + 4 * hi);
+    if constexpr (EPI == EPI_BIAS_RES_F32) {
+        f32x4 rv[NJ][4];                       // all residual loads in flight at once
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+                rv[j][g] = *(const f32x4 *)(res + (size_t)(mrow + 32 * j) * N + nw + 4 * hi + 8 * g);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const size_t rowo = (size_t)(mrow + 32 * j) * N + nw + 4 * hi;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                f32x4 o;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[e] = rv[j][g][e] + (bb[g][e] + acc[j][4 * g + e]);
+                *(f32x4 *)((float *)out + rowo + 8 * g) = o;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            uint32_t pk[4][2];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                h16 o[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float v = bb[g][e] + acc[j][4 * g + e];
+                    o[e] = EPI == EPI_BIAS_GELU_F16 ? gelu_era(v) : (h16)v;
+                }
+                pk[g][0] = __builtin_bit_cast(uint32_t, h16x2{o[0], o[1]});
+                pk[g][1] = __builtin_bit_cast(uint32_t, h16x2{o[2], o[3]});
+            }
+            h16 *orow = (h16 *)out + (size_t)(mrow + 32 * j) * N + nw + 8 * hi;
+#pragma unroll
+            for (int g = 0; g < 4; g += 2) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const auto r2 = __builtin_amdgcn_permlane32_swap(pk[g][h], pk[g + 1][h], false, false);
+                    pk[g][h] = r2[0];
+                    pk[g + 1][h] = r2[1];
+                }
+                uint4 v;
+                v.x = pk[g][0]; v.y = pk[g][1]; v.z = pk[g + 1][0]; v.w = pk[g + 1][1];
+                *(uint4 *)(orow + 8 * g) = v;
+            }
+        }
+    }
+}
+
+template <int FMT, int BM>
+void dispatch_qv(const DevWeight &W, const h16 *x, int M, const float *bias, int epi, const float *res, void *out,
+                 hipStream_t s)
+{
+    const int nN = (W.N + 127) / 128, nTiles = (M / BM) * nN;
+    if (epi == EPI_BIAS_F16)
+        gemmqv_kernel<FMT, EPI_BIAS_F16, BM><<<nTiles, 256, 0, s>>>(W, x, bias, res, out, nN, nTiles);
+    else if (epi == EPI_BIAS_GELU_F16)
+        gemmqv_kernel<FMT, EPI_BIAS_GELU_F16, BM><<<nTiles, 256, 0, s>>>(W, x, bias, res, out, nN, nTiles);
+    else
+        gemmqv_kernel<FMT, EPI_BIAS_RES_F32, BM><<<nTiles, 256, 0, s>>>(W, x, bias, res, out, nN, nTiles);
 }
 
 }  // namespace
 
-// Diagnostic: f16-weight / EPI_BIAS_F16 GEMM with ablation switches, tile 128 or 256.
-template <int BN, int ABL>
-static void abl_one(const DevWeight &W, const h16 *x, int M, const float *bias, void *out, hipStream_t s)
+// Diagnostics: q4_0 gemmqw with per-wave s_memtime stamps (4 per wave) into `stamps`
+// (device buffer of nTiles * 8 * 4 uint64).  Returns the tile count.
+int launch_gemm_q_stamped(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi,
+                          const float *res, void *out, hipStream_t s, int32_t wm, uint64_t *stamps, int32_t diag)
 {
-    const int nN = (W.N + BN - 1) / BN, nTiles = (M / GM) * nN;
-    gemm_kernel<FMT_F16, EPI_BIAS_F16, BN, ABL><<<nTiles, 512, 0, s>>>(W, x, bias, nullptr, out, nN, nTiles);
-}
-
-template <int BN>
-static void abl_bn(const DevWeight &W, const h16 *x, int M, const float *bias, void *out, hipStream_t s, int abl)
-{
-    switch (abl) {
-    case 0: abl_one<BN, 0>(W, x, M, bias, out, s); break;
-    case 1: abl_one<BN, 1>(W, x, M, bias, out, s); break;
-    case 2: abl_one<BN, 2>(W, x, M, bias, out, s); break;
-    case 3: abl_one<BN, 3>(W, x, M, bias, out, s); break;
-    case 4: abl_one<BN, 4>(W, x, M, bias, out, s); break;
-    case 6: abl_one<BN, 6>(W, x, M, bias, out, s); break;
-    case 8: abl_one<BN, 8>(W, x, M, bias, out, s); break;
-    case 11: abl_one<BN, 11>(W, x, M, bias, out, s); break;
-    default: abl_one<BN, 15>(W, x, M, bias, out, s); break;
+    const h16 *x = (const h16 *)X;
+    const int BN = 256 / wm;
+    if (wm == 1) {
+        switch (diag) {
+        case 1: dispatch_qw<FMT_Q4_0, 1, 0x11>(W, x, M, bias, epi, res, out, s, stamps); break;
+        case 2: dispatch_qw<FMT_Q4_0, 1, 0x12>(W, x, M, bias, epi, res, out, s, stamps); break;
+        case 3: dispatch_qw<FMT_Q4_0, 1, 0x13>(W, x, M, bias, epi, res, out, s, stamps); break;
+        case 4: dispatch_qw<FMT_Q4_0, 1, 0x14>(W, x, M, bias, epi, res, out, s, stamps); break;
+        case 8: dispatch_qw<FMT_Q4_0, 1, 0x18>(W, x, M, bias, epi, res, out, s, stamps); break;
+        case 15: dispatch_qw<FMT_Q4_0, 1, 0x1f>(W, x, M, bias, epi, res, out, s, stamps); break;
+        case 32: dispatch_qw<FMT_Q4_0, 1, 0x30>(W, x, M, bias, epi, res, out, s, stamps); break;
+        case 36: dispatch_qw<FMT_Q4_0, 1, 0x34>(W, x, M, bias, epi, res, out, s, stamps); break;
+        default: dispatch_qw<FMT_Q4_0, 1, 0x10>(W, x, M, bias, epi, res, out, s, stamps); break;
+        }
+    } else {
+        dispatch_qw<FMT_Q4_0, 2, 0x10>(W, x, M, bias, epi, res, out, s, stamps);
     }
+    return (M / GM) * ((W.N + BN - 1) / BN);
 }
 
-void launch_gemm_ablation(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, void *out,
-                          hipStream_t s, int32_t abl, int32_t bn)
+int g_gemm_variant = 0;   // 0: heuristic (gemmqv, gemmqw for the GELU form), 2: gemmqw -- A/B benches
+int g_force_bn = 0;       // tests: force the tile shape (128 / 256; 0 = heuristic)
+
+template <int FMT>
+void launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, int32_t epi, const float *res,
+                void *out, hipStream_t s)
 {
-    if (bn == 256) abl_bn<256>(W, (const h16 *)X, M, bias, out, s, abl);
-    else abl_bn<128>(W, (const h16 *)X, M, bias, out, s, abl);
+    const int force = g_force_bn;
+    int variant = g_gemm_variant;
+    // measured (profiles/r01_gemm_sweep.log): the GELU form is fastest as gemmqw
+    // (one 8-wave workgroup per CU), the others as gemmqv (two per CU)
+    if (variant == 0 && epi == EPI_BIAS_GELU_F16 && !force && W.N % 256 == 0 &&
+        (long)(M / GM) * (W.N / 256) >= 512)
+        variant = 2;
+    if (variant == 2) {
+        const bool wide = force ? force == 256 : (W.N % 256 == 0 && (long)(M / GM) * (W.N / 256) >= 512);
+        if (wide) dispatch_qw<FMT, 1>(W, x, M, bias, epi, res, out, s);
+        else dispatch_qw<FMT, 2>(W, x, M, bias, epi, res, out, s);
+        return;
+    }
+    // 2 workgroups / CU; BM 128 for the residual (f32) form and for small M
+    const bool big = force ? force == 256 : (epi != EPI_BIAS_RES_F32 && M >= 256 * 64);
+    if (big) dispatch_qv<FMT, 256>(W, x, M, bias, epi, res, out, s);
+    else dispatch_qv<FMT, 128>(W, x, M, bias, epi, res, out, s);
 }
 
 void launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi, const float *res,
                  void *out, hipStream_t s)
 {
-    if (W.fmt == FMT_Q4_0 || W.fmt == FMT_Q4_1 || W.fmt == FMT_Q8_0)
-        launch_gemm_q(W, X, M, bias, epi, res, out, s, g_force_bn);   // weights in registers (gemm_q.hip)
-    else
-        dispatch<FMT_F16>(W, X, M, bias, epi, res, out, s);
+    const h16 *x = (const h16 *)X;
+    switch (W.fmt) {
+    case FMT_Q4_0: launch_fmt<FMT_Q4_0>(W, x, M, bias, epi, res, out, s); break;
+    case FMT_Q4_1: launch_fmt<FMT_Q4_1>(W, x, M, bias, epi, res, out, s); break;
+    case FMT_Q8_0: launch_fmt<FMT_Q8_0>(W, x, M, bias, epi, res, out, s); break;
+    default: launch_fmt<FMT_F16>(W, x, M, bias, epi, res, out, s); break;
+    }
 }
 
 }  // namespace emb

@@ -5,7 +5,9 @@
 //            blocks): element (n, k) lives in step ks = k/64 at
 //            ((ks*N + n) * 64 + k%64) -- one K-step of a 128-row tile is one
 //            contiguous, fully coalesced run of bytes.
-//              f16 : 128 B per (ks, n), k ascending (LDS-staged GEMM)
+//              f16 : 128 B per (ks, n) in MFMA A-fragment order: byte
+//                    64h + 16kk + 2i holds k = 16kk + 8h + i (the lane of
+//                    half h loads its 4 fragments as 64 contiguous bytes)
 //              q4_0/q4_1: 32 B nibbles per (ks, n) in the MFMA A-fragment
 //                    ("register") order of gemm_q.hip: word 4h + kk holds
 //                    k = 16kk + 8h + i (i = 0..7), element i at bit
@@ -54,23 +56,14 @@ constexpr int ATT_QT = 128;           // queries per attention workgroup
 void launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi,
                  const float *res, void *out, hipStream_t s);
 
-// Quantized-weight GEMM (gemm_q.hip); force_bn: 0 = heuristic, 128 / 256.
-void launch_gemm_q(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi,
-                   const float *res, void *out, hipStream_t s, int32_t force_bn);
-
-// Tests only: force the GEMM tile width (128 / 256; 0 = heuristic).
+// Tests only: force the GEMM tile shape (128 / 256; 0 = heuristic).
 extern int g_force_bn;
-// Benches only: quantized GEMM kernel variant (0 = gemmqw, 1 = gemmq).
+// Benches only: GEMM kernel variant (0 = heuristic, 2 = gemmqw everywhere).
 extern int g_gemm_variant;
 // Diagnostics: q4_0 gemmqw (wm waves along tokens) with per-wave s_memtime stamps.
 int launch_gemm_q_stamped(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi,
                           const float *res, void *out, hipStream_t s, int32_t wm, uint64_t *stamps,
                           int32_t diag);
-
-// Diagnostics only: q4_0 GEMM with parts switched off (1 no per-step loads,
-// 2 no dequant, 4 no MFMA, 8 no epilogue; combinations 3, 6, 11, 15).
-void launch_gemm_ablation(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, void *out,
-                          hipStream_t s, int32_t abl, int32_t bn);
 
 // x = LN(pos[i] + (type[0] + word[id])) for every valid token (bert.cpp:963-984).
 void launch_embed_ln(const DevTable &word, const DevTable &type, const DevTable &pos, const float *ln_w,

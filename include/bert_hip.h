@@ -72,8 +72,11 @@ BERT_API int32_t bertx_test_gemm(int32_t fmt, int32_t N, int32_t K, const void *
 /*
  * GEMM micro-benchmark on random operands (device 0): average device time of
  * `iters` launches of the production GEMM for fmt / N / K / M / epi (tile_n 0 =
- * production choice).  ablate >= 0 selects a diagnostic q4_0 build with parts
- * switched off (1 per-step loads, 2 dequant, 4 MFMA, 8 epilogue; 3, 6, 11, 15).
+ * production choice).  ablate: -1 = production kernels; -2 = the one-workgroup-
+ * per-CU kernel (gemmqw) for every form; -3 - d (q4_0 only) = one extra launch of
+ * a diagnostic gemmqw build with per-wave s_memtime phase stamps (printed to
+ * stderr) and ablation bits d (1 no dequant, 2 no B reads, 4 no K-loop barrier,
+ * 8 no MFMA, 32 sched-group pipelined).
  */
 BERT_API int32_t bertx_bench_gemm(int32_t fmt, int32_t N, int32_t K, int32_t M, int32_t epi, int32_t tile_n,
                                   int32_t ablate, int32_t iters, float *avg_us);

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """GEMM micro-benchmark sweep (device-timed, random operands): production
-configurations of the bge-base forward and ablation builds.  Prints one line per
+configurations of the bge-base forward, production vs gemmqw.  Prints one line per
 case: name, avg us, TFLOP/s."""
 import ctypes
 import os
@@ -13,8 +13,9 @@ import bertpy  # noqa: E402
 L = bertpy.load_lib()
 M = int(os.environ.get("SWEEP_M", "32768"))
 cases = [("qkv", 2, 2304, 768, 0), ("attn_out", 2, 768, 768, 2), ("ffn_up", 2, 3072, 768, 1),
-         ("ffn_down", 2, 768, 3072, 2), ("ffn_up_q8", 8, 3072, 768, 1), ("ffn_up_q41", 3, 3072, 768, 1)]
-variants = [("qv", -1), ("old", -2), ("qw", -4)]
+         ("ffn_down", 2, 768, 3072, 2), ("ffn_up_q8", 8, 3072, 768, 1), ("ffn_up_q41", 3, 3072, 768, 1),
+         ("ffn_up_f16", 1, 3072, 768, 1), ("qkv_f16", 1, 2304, 768, 0), ("ffn_down_f16", 1, 768, 3072, 2)]
+variants = [("prod", -1), ("qw", -2)]
 for rnd in range(int(os.environ.get("SWEEP_ROUNDS", "2"))):
     for name, fmt, N, K, epi in cases:
         for vname, abl in variants:
