@@ -282,7 +282,7 @@ bool Device::reserve(int64_t tokens, int64_t seqs)
     const int64_t d = hp_.n_embd, f = hp_.n_intermediate;
     size_t off = 0;
     auto take = [&](size_t bytes) { size_t o = off; off += align_up(bytes, 256); return o; };
-    const size_t o_x32 = take(rows * d * 4), o_y32 = take(rows * d * 4), o_xh = take(rows * d * 2);
+    const size_t o_st = take(rows * 8), o_y32 = take(rows * d * 4), o_xh = take(rows * d * 2);
     const size_t o_qkv = take(rows * 3 * d * 2), o_att = take(rows * d * 2), o_ffn = take(rows * f * 2);
     const size_t o_ids = take(rows * 4), o_cu = take((ns + 1) * 4), o_out = take(ns * d * 4);
     const size_t o_pool = take((size_t)ns * pool_chunks(hp_.n_max_tokens) * d * 4);
@@ -296,7 +296,7 @@ bool Device::reserve(int64_t tokens, int64_t seqs)
     // be ordered before the forward that follows on stream_
     HIP_OK(hipMemsetAsync(ws_, 0, off, stream_));
     HIP_OK(hipStreamSynchronize(stream_));
-    x32_ = (float *)(ws_ + o_x32); y32_ = (float *)(ws_ + o_y32); xh_ = (uint16_t *)(ws_ + o_xh);
+    st_ = (float2 *)(ws_ + o_st); y32_ = (float *)(ws_ + o_y32); xh_ = (uint16_t *)(ws_ + o_xh);
     qkv_ = (uint16_t *)(ws_ + o_qkv); att_ = (uint16_t *)(ws_ + o_att); ffn_ = (uint16_t *)(ws_ + o_ffn);
     d_ids_ = (int32_t *)(ws_ + o_ids); d_cu_ = (int32_t *)(ws_ + o_cu); d_out_ = (float *)(ws_ + o_out);
     pool_part_ = (float *)(ws_ + o_pool);
@@ -386,9 +386,12 @@ int Device::forward(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, int m
     };
 
     begin(K_EMBED_LN, s, ev);
-    launch_embed_ln(word_, type_, pos_, ln_e_w_, ln_e_b_, d_ids, d_cu, n_seqs, max_len, d, x32_, xh_, s);
+    launch_embed_ln(word_, type_, pos_, ln_e_w_, ln_e_b_, d_ids, d_cu, n_seqs, max_len, d, y32_, xh_, st_, s);
     end(K_EMBED_LN, s, ev, t * (4.0 + 3.0 * d * 2.0 + 6.0 * d));
-    chk("embed_ln", -1, x32_, (size_t)T * d, 0);
+    chk("embed_ln", -1, xh_, (size_t)T * d, 1);
+    // the residual stream stays pre-LN; `prev` is the LN that normalises it
+    ResLN prev;
+    prev.stats = st_; prev.w = ln_e_w_; prev.b = ln_e_b_;
 
     const double att_flop = 4.0 * (double)d * t * (double)max_len;   // exact when all lengths are equal
     for (int l = 0; l < hp_.n_layer; ++l) {
@@ -404,14 +407,15 @@ int Device::forward(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, int m
         chk("attention", l, att_, (size_t)T * d, 1);
 
         begin(K_GEMM_O, s, ev);
-        launch_gemm(L.o, att_, M, L.b_o, EPI_BIAS_RES_F32, x32_, y32_, s);
+        launch_gemm(L.o, att_, M, L.b_o, EPI_BIAS_RES_F32, y32_, y32_, s, prev);
         end(K_GEMM_O, s, ev, 2.0 * t * d * d);
         chk("gemm_o", l, y32_, (size_t)T * d, 0);
 
         begin(K_LAYERNORM, s, ev);
-        launch_layernorm(y32_, T, d, L.ln1_w, L.ln1_b, x32_, xh_, s);
+        launch_layernorm(y32_, T, d, L.ln1_w, L.ln1_b, xh_, st_, s);
+        prev.w = L.ln1_w; prev.b = L.ln1_b;
         end(K_LAYERNORM, s, ev, t * d * 10.0);
-        chk("layernorm1", l, x32_, (size_t)T * d, 0);
+        chk("layernorm1", l, xh_, (size_t)T * d, 1);
 
         begin(K_GEMM_FFN_UP, s, ev);
         launch_gemm(L.up, xh_, M, L.b_up, EPI_BIAS_GELU_F16, nullptr, ffn_, s);
@@ -419,17 +423,18 @@ int Device::forward(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, int m
         chk("gemm_up", l, ffn_, (size_t)T * f, 1);
 
         begin(K_GEMM_FFN_DOWN, s, ev);
-        launch_gemm(L.down, ffn_, M, L.b_down, EPI_BIAS_RES_F32, x32_, y32_, s);
+        launch_gemm(L.down, ffn_, M, L.b_down, EPI_BIAS_RES_F32, y32_, y32_, s, prev);
         end(K_GEMM_FFN_DOWN, s, ev, 2.0 * t * d * f);
         chk("gemm_down", l, y32_, (size_t)T * d, 0);
 
         begin(K_LAYERNORM, s, ev);
-        launch_layernorm(y32_, T, d, L.ln2_w, L.ln2_b, x32_, xh_, s);
+        launch_layernorm(y32_, T, d, L.ln2_w, L.ln2_b, xh_, st_, s);
+        prev.w = L.ln2_w; prev.b = L.ln2_b;
         end(K_LAYERNORM, s, ev, t * d * 10.0);
-        chk("layernorm2", l, x32_, (size_t)T * d, 0);
+        chk("layernorm2", l, xh_, (size_t)T * d, 1);
     }
     begin(K_POOL_L2, s, ev);
-    launch_pool_l2(x32_, d_cu, n_seqs, max_len, d, pool_part_, d_out, s);
+    launch_pool_l2(y32_, prev, d_cu, n_seqs, max_len, d, pool_part_, d_out, s);
     end(K_POOL_L2, s, ev, t * d * 4.0 + (double)n_seqs * d * 4.0);
     chk("pool_l2", -1, d_out, (size_t)n_seqs * d, 0);
     if (cnt) (void)hipFree(cnt);

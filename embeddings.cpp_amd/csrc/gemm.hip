@@ -171,7 +171,7 @@ constexpr int qrec_bytes() { return FMT == FMT_F16 ? 128 : FMT == FMT_Q8_0 ? 64 
 template <int FMT, int EPI, int WM, int DIAG = 0>
 __global__ __launch_bounds__(512, 1) void gemmqw_kernel(DevWeight W, const h16 *__restrict__ X,
                                                         const float *__restrict__ bias, const float *__restrict__ res,
-                                                        void *__restrict__ out, int nN, int nTiles,
+                                                        void *__restrict__ out, int nN, int nTiles, ResLN rln,
                                                         uint64_t *__restrict__ stamps = nullptr)
 {
     // STAMP (diagnostics build only): s_memtime at start / after the prologue /
@@ -332,12 +332,27 @@ __global__ __launch_bounds__(512, 1) void gemmqw_kernel(DevWeight W, const h16 *
 #pragma unroll
     for (int g = 0; g < 4; ++g) bb[g] = *(const f32x4 *)(bias + nw + 8 * g + 4 * hi);
     if constexpr (EPI == EPI_BIAS_RES_F32) {
+        f32x4 lw[4], lb[4];
+        if (rln.stats) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                lw[g] = *(const f32x4 *)(rln.w + nw + 8 * g + 4 * hi);
+                lb[g] = *(const f32x4 *)(rln.b + nw + 8 * g + 4 * hi);
+            }
+        }
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             const size_t rowo = (size_t)(mrow + 32 * j) * N + nw + 4 * hi;
             f32x4 rv[4];
 #pragma unroll
             for (int g = 0; g < 4; ++g) rv[g] = *(const f32x4 *)(res + rowo + 8 * g);
+            if (rln.stats) {                   // residual = LN(pre-LN row), recomputed
+                const float2 st = rln.stats[mrow + 32 * j];
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) rv[g][e] = ln_apply(rv[g][e], st.x, st.y, lw[g][e], lb[g][e]);
+            }
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 f32x4 o;
@@ -387,17 +402,17 @@ __global__ __launch_bounds__(512, 1) void gemmqw_kernel(DevWeight W, const h16 *
 
 template <int FMT, int WM, int STAMP = 0>
 void dispatch_qw(const DevWeight &W, const h16 *x, int M, const float *bias, int epi, const float *res, void *out,
-                 hipStream_t s, uint64_t *stamps = nullptr)
+                 hipStream_t s, const ResLN &rln, uint64_t *stamps = nullptr)
 {
     constexpr int BN = 256 / WM;
     const int nN = (W.N + BN - 1) / BN, nTiles = (M / GM) * nN;
     if (epi == EPI_BIAS_F16)
-        gemmqw_kernel<FMT, EPI_BIAS_F16, WM, STAMP><<<nTiles, 512, 0, s>>>(W, x, bias, res, out, nN, nTiles, stamps);
+        gemmqw_kernel<FMT, EPI_BIAS_F16, WM, STAMP><<<nTiles, 512, 0, s>>>(W, x, bias, res, out, nN, nTiles, rln, stamps);
     else if (epi == EPI_BIAS_GELU_F16)
-        gemmqw_kernel<FMT, EPI_BIAS_GELU_F16, WM, STAMP><<<nTiles, 512, 0, s>>>(W, x, bias, res, out, nN, nTiles,
+        gemmqw_kernel<FMT, EPI_BIAS_GELU_F16, WM, STAMP><<<nTiles, 512, 0, s>>>(W, x, bias, res, out, nN, nTiles, rln,
                                                                               stamps);
     else
-        gemmqw_kernel<FMT, EPI_BIAS_RES_F32, WM, STAMP><<<nTiles, 512, 0, s>>>(W, x, bias, res, out, nN, nTiles,
+        gemmqw_kernel<FMT, EPI_BIAS_RES_F32, WM, STAMP><<<nTiles, 512, 0, s>>>(W, x, bias, res, out, nN, nTiles, rln,
                                                                              stamps);
 }
 
@@ -414,7 +429,7 @@ void dispatch_qw(const DevWeight &W, const h16 *x, int M, const float *bias, int
 template <int FMT, int EPI, int BM>
 __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemmqv_kernel(DevWeight W, const h16 *__restrict__ X,
                                                         const float *__restrict__ bias, const float *__restrict__ res,
-                                                        void *__restrict__ out, int nN, int nTiles)
+                                                        void *__restrict__ out, int nN, int nTiles, ResLN rln)
 {
     constexpr int BN = 128;
     constexpr int NJ = BM / 32;
@@ -531,6 +546,22 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 #pragma unroll
             for (int g = 0; g < 4; ++g)
                 rv[j][g] = *(const f32x4 *)(res + (size_t)(mrow + 32 * j) * N + nw + 4 * hi + 8 * g);
+        if (rln.stats) {                       // residual = LN(pre-LN row), recomputed
+            f32x4 lw[4], lb[4];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                lw[g] = *(const f32x4 *)(rln.w + nw + 8 * g + 4 * hi);
+                lb[g] = *(const f32x4 *)(rln.b + nw + 8 * g + 4 * hi);
+            }
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const float2 st = rln.stats[mrow + 32 * j];
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) rv[j][g][e] = ln_apply(rv[j][g][e], st.x, st.y, lw[g][e], lb[g][e]);
+            }
+        }
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             const size_t rowo = (size_t)(mrow + 32 * j) * N + nw + 4 * hi;
@@ -576,15 +607,15 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 
 template <int FMT, int BM>
 void dispatch_qv(const DevWeight &W, const h16 *x, int M, const float *bias, int epi, const float *res, void *out,
-                 hipStream_t s)
+                 hipStream_t s, const ResLN &rln)
 {
     const int nN = (W.N + 127) / 128, nTiles = (M / BM) * nN;
     if (epi == EPI_BIAS_F16)
-        gemmqv_kernel<FMT, EPI_BIAS_F16, BM><<<nTiles, 256, 0, s>>>(W, x, bias, res, out, nN, nTiles);
+        gemmqv_kernel<FMT, EPI_BIAS_F16, BM><<<nTiles, 256, 0, s>>>(W, x, bias, res, out, nN, nTiles, rln);
     else if (epi == EPI_BIAS_GELU_F16)
-        gemmqv_kernel<FMT, EPI_BIAS_GELU_F16, BM><<<nTiles, 256, 0, s>>>(W, x, bias, res, out, nN, nTiles);
+        gemmqv_kernel<FMT, EPI_BIAS_GELU_F16, BM><<<nTiles, 256, 0, s>>>(W, x, bias, res, out, nN, nTiles, rln);
     else
-        gemmqv_kernel<FMT, EPI_BIAS_RES_F32, BM><<<nTiles, 256, 0, s>>>(W, x, bias, res, out, nN, nTiles);
+        gemmqv_kernel<FMT, EPI_BIAS_RES_F32, BM><<<nTiles, 256, 0, s>>>(W, x, bias, res, out, nN, nTiles, rln);
 }
 
 }  // namespace
@@ -598,18 +629,18 @@ int launch_gemm_q_stamped(const DevWeight &W, const uint16_t *X, int32_t M, cons
     const int BN = 256 / wm;
     if (wm == 1) {
         switch (diag) {
-        case 1: dispatch_qw<FMT_Q4_0, 1, 0x11>(W, x, M, bias, epi, res, out, s, stamps); break;
-        case 2: dispatch_qw<FMT_Q4_0, 1, 0x12>(W, x, M, bias, epi, res, out, s, stamps); break;
-        case 3: dispatch_qw<FMT_Q4_0, 1, 0x13>(W, x, M, bias, epi, res, out, s, stamps); break;
-        case 4: dispatch_qw<FMT_Q4_0, 1, 0x14>(W, x, M, bias, epi, res, out, s, stamps); break;
-        case 8: dispatch_qw<FMT_Q4_0, 1, 0x18>(W, x, M, bias, epi, res, out, s, stamps); break;
-        case 15: dispatch_qw<FMT_Q4_0, 1, 0x1f>(W, x, M, bias, epi, res, out, s, stamps); break;
-        case 32: dispatch_qw<FMT_Q4_0, 1, 0x30>(W, x, M, bias, epi, res, out, s, stamps); break;
-        case 36: dispatch_qw<FMT_Q4_0, 1, 0x34>(W, x, M, bias, epi, res, out, s, stamps); break;
-        default: dispatch_qw<FMT_Q4_0, 1, 0x10>(W, x, M, bias, epi, res, out, s, stamps); break;
+        case 1: dispatch_qw<FMT_Q4_0, 1, 0x11>(W, x, M, bias, epi, res, out, s, ResLN(), stamps); break;
+        case 2: dispatch_qw<FMT_Q4_0, 1, 0x12>(W, x, M, bias, epi, res, out, s, ResLN(), stamps); break;
+        case 3: dispatch_qw<FMT_Q4_0, 1, 0x13>(W, x, M, bias, epi, res, out, s, ResLN(), stamps); break;
+        case 4: dispatch_qw<FMT_Q4_0, 1, 0x14>(W, x, M, bias, epi, res, out, s, ResLN(), stamps); break;
+        case 8: dispatch_qw<FMT_Q4_0, 1, 0x18>(W, x, M, bias, epi, res, out, s, ResLN(), stamps); break;
+        case 15: dispatch_qw<FMT_Q4_0, 1, 0x1f>(W, x, M, bias, epi, res, out, s, ResLN(), stamps); break;
+        case 32: dispatch_qw<FMT_Q4_0, 1, 0x30>(W, x, M, bias, epi, res, out, s, ResLN(), stamps); break;
+        case 36: dispatch_qw<FMT_Q4_0, 1, 0x34>(W, x, M, bias, epi, res, out, s, ResLN(), stamps); break;
+        default: dispatch_qw<FMT_Q4_0, 1, 0x10>(W, x, M, bias, epi, res, out, s, ResLN(), stamps); break;
         }
     } else {
-        dispatch_qw<FMT_Q4_0, 2, 0x10>(W, x, M, bias, epi, res, out, s, stamps);
+        dispatch_qw<FMT_Q4_0, 2, 0x10>(W, x, M, bias, epi, res, out, s, ResLN(), stamps);
     }
     return (M / GM) * ((W.N + BN - 1) / BN);
 }
@@ -619,7 +650,7 @@ int g_force_bn = 0;       // tests: force the tile shape (128 / 256; 0 = heurist
 
 template <int FMT>
 void launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, int32_t epi, const float *res,
-                void *out, hipStream_t s)
+                void *out, hipStream_t s, const ResLN &rln)
 {
     const int force = g_force_bn;
     int variant = g_gemm_variant;
@@ -630,25 +661,25 @@ void launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, 
         variant = 2;
     if (variant == 2) {
         const bool wide = force ? force == 256 : (W.N % 256 == 0 && (long)(M / GM) * (W.N / 256) >= 512);
-        if (wide) dispatch_qw<FMT, 1>(W, x, M, bias, epi, res, out, s);
-        else dispatch_qw<FMT, 2>(W, x, M, bias, epi, res, out, s);
+        if (wide) dispatch_qw<FMT, 1>(W, x, M, bias, epi, res, out, s, rln);
+        else dispatch_qw<FMT, 2>(W, x, M, bias, epi, res, out, s, rln);
         return;
     }
     // 2 workgroups / CU; BM 128 for the residual (f32) form and for small M
     const bool big = force ? force == 256 : (epi != EPI_BIAS_RES_F32 && M >= 256 * 64);
-    if (big) dispatch_qv<FMT, 256>(W, x, M, bias, epi, res, out, s);
-    else dispatch_qv<FMT, 128>(W, x, M, bias, epi, res, out, s);
+    if (big) dispatch_qv<FMT, 256>(W, x, M, bias, epi, res, out, s, rln);
+    else dispatch_qv<FMT, 128>(W, x, M, bias, epi, res, out, s, rln);
 }
 
 void launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi, const float *res,
-                 void *out, hipStream_t s)
+                 void *out, hipStream_t s, const ResLN &rln)
 {
     const h16 *x = (const h16 *)X;
     switch (W.fmt) {
-    case FMT_Q4_0: launch_fmt<FMT_Q4_0>(W, x, M, bias, epi, res, out, s); break;
-    case FMT_Q4_1: launch_fmt<FMT_Q4_1>(W, x, M, bias, epi, res, out, s); break;
-    case FMT_Q8_0: launch_fmt<FMT_Q8_0>(W, x, M, bias, epi, res, out, s); break;
-    default: launch_fmt<FMT_F16>(W, x, M, bias, epi, res, out, s); break;
+    case FMT_Q4_0: launch_fmt<FMT_Q4_0>(W, x, M, bias, epi, res, out, s, rln); break;
+    case FMT_Q4_1: launch_fmt<FMT_Q4_1>(W, x, M, bias, epi, res, out, s, rln); break;
+    case FMT_Q8_0: launch_fmt<FMT_Q8_0>(W, x, M, bias, epi, res, out, s, rln); break;
+    default: launch_fmt<FMT_F16>(W, x, M, bias, epi, res, out, s, rln); break;
     }
 }
 

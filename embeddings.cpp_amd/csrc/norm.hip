@@ -50,9 +50,12 @@ __device__ __forceinline__ f32x4 table4(const DevTable &t, int row, int c)
     }
 }
 
-// ggml_norm (eps 1e-5, mean then centred variance) * w + b, bert.cpp:977-984
-__device__ __forceinline__ void ln_row(f32x4 (&v)[MAXV], int d, int lane, const float *w, const float *b, float *x32,
-                                       h16 *xh)
+// ggml_norm (eps 1e-5, mean then centred variance) * w + b, bert.cpp:977-984.
+// Writes the f16 GEMM input and the row's (mean, 1/sigma); the f32 normalised
+// row itself is not stored -- the next residual epilogue recomputes it from the
+// pre-LN row with ln_apply (kernels.h), the same expression as here.
+__device__ __forceinline__ void ln_row(f32x4 (&v)[MAXV], int d, int lane, const float *w, const float *b, h16 *xh,
+                                       float2 *st)
 {
     float s = 0.f;
 #pragma unroll
@@ -67,7 +70,7 @@ __device__ __forceinline__ void ln_row(f32x4 (&v)[MAXV], int d, int lane, const 
         const int c = 4 * (lane + 64 * k);
         if (c < d) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) { v[k][e] -= mean; s2 += v[k][e] * v[k][e]; }
+            for (int e = 0; e < 4; ++e) { const float u = v[k][e] - mean; s2 += u * u; }
         }
     }
     const float scale = 1.0f / sqrtf(wave_sum(s2) / (float)d + 1e-5f);
@@ -76,19 +79,19 @@ __device__ __forceinline__ void ln_row(f32x4 (&v)[MAXV], int d, int lane, const 
         const int c = 4 * (lane + 64 * k);
         if (c >= d) continue;
         const f32x4 ww = *(const f32x4 *)(w + c), bb = *(const f32x4 *)(b + c);
-        f32x4 y;
         h16x4 yh;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) { y[e] = ww[e] * (v[k][e] * scale) + bb[e]; yh[e] = (h16)y[e]; }
-        *(f32x4 *)(x32 + c) = y;
+        for (int e = 0; e < 4; ++e) yh[e] = (h16)ln_apply(v[k][e], mean, scale, ww[e], bb[e]);
         *(h16x4 *)(xh + c) = yh;
     }
+    if (lane == 0) *st = float2{mean, scale};
 }
 
 __global__ __launch_bounds__(256) void embed_ln_kernel(DevTable word, DevTable type, DevTable pos,
                                                        const float *__restrict__ ln_w, const float *__restrict__ ln_b,
                                                        const int32_t *__restrict__ ids, const int32_t *__restrict__ cu,
-                                                       int d, float *__restrict__ x32, h16 *__restrict__ xh)
+                                                       int d, float *__restrict__ y32, h16 *__restrict__ xh,
+                                                       float2 *__restrict__ stats)
 {
     const int b = blockIdx.y, lane = threadIdx.x & 63;
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -104,14 +107,15 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(DevTable word, DevTable t
             const f32x4 w = table4(word, id, c), ty = table4(type, 0, c), p = table4(pos, i, c);
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[k][e] = p[e] + (ty[e] + w[e]);
+            *(f32x4 *)(y32 + (size_t)t * d + c) = v[k];          // pre-LN residual stream
         }
     }
-    ln_row(v, d, lane, ln_w, ln_b, x32 + (size_t)t * d, xh + (size_t)t * d);
+    ln_row(v, d, lane, ln_w, ln_b, xh + (size_t)t * d, stats + t);
 }
 
 __global__ __launch_bounds__(256) void layernorm_kernel(const float *__restrict__ y, int T, int d,
                                                         const float *__restrict__ w, const float *__restrict__ b,
-                                                        float *__restrict__ x32, h16 *__restrict__ xh)
+                                                        h16 *__restrict__ xh, float2 *__restrict__ stats)
 {
     const int lane = threadIdx.x & 63;
     const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -123,15 +127,17 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float *__restrict_
         const int c = 4 * (lane + 64 * k);
         if (c < d) v[k] = *(const f32x4 *)(row + c);
     }
-    ln_row(v, d, lane, w, b, x32 + (size_t)t * d, xh + (size_t)t * d);
+    ln_row(v, d, lane, w, b, xh + (size_t)t * d, stats + t);
 }
 
 // pool stage 1: partial column sums of 64-token chunks, weights 1/len
 // (bert.cpp:1087-1089: sum_i X[i][c] * (1/len)).
 constexpr int POOL_CHUNK = 64;
 
-__global__ __launch_bounds__(256) void pool_partial_kernel(const float *__restrict__ x32, const int32_t *__restrict__ cu,
-                                                           int d, int n_chunks, float *__restrict__ part)
+__global__ __launch_bounds__(256) void pool_partial_kernel(const float *__restrict__ y32, const float2 *__restrict__ stats,
+                                                           const float *__restrict__ lw, const float *__restrict__ lb,
+                                                           const int32_t *__restrict__ cu, int d, int n_chunks,
+                                                           float *__restrict__ part)
 {
     const int b = blockIdx.y, ch = blockIdx.x;
     const int start = cu[b], len = cu[b + 1] - start;
@@ -140,10 +146,13 @@ __global__ __launch_bounds__(256) void pool_partial_kernel(const float *__restri
     const float wt = 1.0f / (float)len;
     for (int c = 4 * threadIdx.x; c < d; c += 4 * 256) {
         f32x4 a = {0.f, 0.f, 0.f, 0.f};
+        const f32x4 ww = *(const f32x4 *)(lw + c), bb = *(const f32x4 *)(lb + c);
         const int i1 = min(len, i0 + POOL_CHUNK);
         for (int i = i0; i < i1; ++i) {
-            const f32x4 x = *(const f32x4 *)(x32 + (size_t)(start + i) * d + c);
-            a[0] += x[0] * wt; a[1] += x[1] * wt; a[2] += x[2] * wt; a[3] += x[3] * wt;
+            const f32x4 y = *(const f32x4 *)(y32 + (size_t)(start + i) * d + c);
+            const float2 st = stats[start + i];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) a[e] += ln_apply(y[e], st.x, st.y, ww[e], bb[e]) * wt;
         }
         *(f32x4 *)(dst + c) = a;
     }
@@ -192,25 +201,25 @@ void launch_count_nonfinite(const void *p, size_t n, int f16, unsigned *cnt, hip
 
 void launch_embed_ln(const DevTable &word, const DevTable &type, const DevTable &pos, const float *ln_w,
                      const float *ln_b, const int32_t *ids, const int32_t *cu, int32_t n_seqs, int32_t max_len,
-                     int32_t d, float *x32, uint16_t *xh, hipStream_t s)
+                     int32_t d, float *y32, uint16_t *xh, float2 *stats, hipStream_t s)
 {
     dim3 grid((max_len + 3) / 4, n_seqs);
-    embed_ln_kernel<<<grid, 256, 0, s>>>(word, type, pos, ln_w, ln_b, ids, cu, d, x32, (h16 *)xh);
+    embed_ln_kernel<<<grid, 256, 0, s>>>(word, type, pos, ln_w, ln_b, ids, cu, d, y32, (h16 *)xh, stats);
 }
 
-void launch_layernorm(const float *y, int32_t T, int32_t d, const float *w, const float *b, float *x32,
-                      uint16_t *xh, hipStream_t s)
+void launch_layernorm(const float *y, int32_t T, int32_t d, const float *w, const float *b, uint16_t *xh,
+                      float2 *stats, hipStream_t s)
 {
-    layernorm_kernel<<<(T + 3) / 4, 256, 0, s>>>(y, T, d, w, b, x32, (h16 *)xh);
+    layernorm_kernel<<<(T + 3) / 4, 256, 0, s>>>(y, T, d, w, b, (h16 *)xh, stats);
 }
 
 int32_t pool_chunks(int32_t max_len) { return (max_len + POOL_CHUNK - 1) / POOL_CHUNK; }
 
-void launch_pool_l2(const float *x32, const int32_t *cu, int32_t n_seqs, int32_t max_len, int32_t d, float *partial,
-                    float *out, hipStream_t s)
+void launch_pool_l2(const float *y32, const ResLN &ln, const int32_t *cu, int32_t n_seqs, int32_t max_len, int32_t d,
+                    float *partial, float *out, hipStream_t s)
 {
     const int nc = pool_chunks(max_len);
-    pool_partial_kernel<<<dim3(nc, n_seqs), 256, 0, s>>>(x32, cu, d, nc, partial);
+    pool_partial_kernel<<<dim3(nc, n_seqs), 256, 0, s>>>(y32, ln.stats, ln.w, ln.b, cu, d, nc, partial);
     pool_final_kernel<<<n_seqs, 256, 0, s>>>(partial, d, nc, out);
 }
 
