@@ -145,11 +145,172 @@ __global__ __launch_bounds__(256) void attention_kernel(const h16 *__restrict__ 
     }
 }
 
+// ---------------------------------------------------------------------------
+// attention_lds: one workgroup per (sentence, head), up to 512 keys.  The
+// sentence's whole K and V (<= 512 x DH f16 each, 128 KiB at DH 64) are
+// brought into LDS ONCE by LDS-DMA; 16 waves x 32 queries then run with no
+// further global loads and no barriers.
+//   K image: [key][DH] rows, 16-B chunks XOR-swizzled by (key & 7) (via the
+//            DMA source address), read as ds_read_b128 A fragments of S^T = K Q^T.
+//   V image: [key][DH] rows, chunks XOR-swizzled by ((key >> 1) & 1) << 2, read
+//            with ds_read_b64_tr_b16 as the transposed A fragments of
+//            O^T += V^T P^T -- no transposing copy.
+// Q is pre-scaled by log2(e)/sqrt(dh) (f16), so S comes out in the exp2 domain;
+// keys past the sentence end are masked (only in the last 64-key block).
+// ---------------------------------------------------------------------------
+template <int DH>
+__global__ __launch_bounds__(1024) void attention_lds_kernel(const h16 *__restrict__ qkv,
+                                                             const int32_t *__restrict__ cu, int d, int nh,
+                                                             float sl2, h16 *__restrict__ out)
+{
+    constexpr int RB = DH * 2, CH = RB / 16, LMAX = ATT_LDS_MAX;
+    __shared__ __attribute__((aligned(16))) char smem[2 * LMAX * RB];
+    char *Kl = smem, *Vl = smem + LMAX * RB;
+    const int h = blockIdx.x % nh, b = blockIdx.x / nh;
+    const int start = cu[b], len = cu[b + 1] - start;
+    if (len <= 0) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int hi = lane >> 5, lq = lane & 31;
+    const int ld = 3 * d;
+    const int nrows = (len + 63) & ~63;
+
+    // ---- K and V of the sentence -> LDS (64 chunks of 16 B per wave-instruction) ----
+    {
+        const int ninstr = nrows * CH / 64;
+        const h16 *kbase = qkv + (size_t)start * ld + d + h * DH;
+        const h16 *vbase = kbase + d;
+        for (int i = w; i < ninstr; i += 16) {
+            const int g = i * 64 + lane, row = g / CH, pc = g % CH;
+            const int srow = min(row, len - 1);          // rows past the end: finite copies, masked / P = 0
+            const int ck = pc ^ (row & (CH - 1));
+            const int cv = pc ^ ((((row >> 1) & 1) << 2) & (CH - 1));
+            glds<16>(kbase + (size_t)srow * ld + ck * 8, Kl + i * 1024);
+            glds<16>(vbase + (size_t)srow * ld + cv * 8, Vl + i * 1024);
+        }
+        wait_vmcnt<0>();
+        __syncthreads();
+    }
+
+    const int q0 = 32 * w;
+    if (q0 >= len) return;                                // no barrier follows
+    const int q = q0 + lq;
+    h16x8 qf[DH / 16];
+    {
+        const h16 *qrow = qkv + (size_t)(start + min(q, len - 1)) * ld + h * DH;
+        const h16 s16 = (h16)sl2;
+        const h16x8 sc = {s16, s16, s16, s16, s16, s16, s16, s16};
+#pragma unroll
+        for (int s = 0; s < DH / 16; ++s) qf[s] = *(const h16x8 *)(qrow + 16 * s + 8 * hi) * sc;
+    }
+    f32x16 o[DH / 32];
+#pragma unroll
+    for (int t = 0; t < DH / 32; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[t][r] = 0.f;
+    float m_i = -INFINITY, l_i = 0.f;
+
+    // tr-read lane roles: group g = lane >> 4 reads rows r0 + (i >> 2), columns c0 + 4 (i & 3)
+    const int gi = lane & 15, gq = gi >> 2, gp = gi & 3, gg = lane >> 4;
+
+    for (int kb = 0; kb < nrows; kb += 64) {
+        f32x16 s[2];
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[kh][r] = 0.f;
+            const int row = kb + 32 * kh + lq;
+            const char *krow = Kl + row * RB;
+#pragma unroll
+            for (int st = 0; st < DH / 16; ++st) {
+                const h16x8 a = *(const h16x8 *)(krow + (((2 * st + hi) ^ (row & (CH - 1))) << 4));
+                s[kh] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, qf[st], s[kh], 0, 0, 0);
+            }
+        }
+        if (kb + 64 > len) {
+#pragma unroll
+            for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int key = kb + 32 * kh + (r & 3) + 8 * (r >> 2) + 4 * hi;
+                    if (key >= len) s[kh][r] = -INFINITY;
+                }
+        }
+        float mx = s[0][0];
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[kh][r]);
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float m_new = fmaxf(m_i, mx);
+        const float alpha = __builtin_amdgcn_exp2f(m_i - m_new);
+        float rs = 0.f;
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float p = __builtin_amdgcn_exp2f(s[kh][r] - m_new);
+                s[kh][r] = p;
+                rs += p;
+            }
+        rs += __shfl_xor(rs, 32, 64);
+        l_i = l_i * alpha + rs;
+        m_i = m_new;
+#pragma unroll
+        for (int t = 0; t < DH / 32; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) {
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                h16x8 bp;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) bp[j] = (h16)s[kh][8 * s2 + j];
+                const int r0 = kb + 32 * kh + 16 * s2 + 4 * (gg >> 1) + gq;
+#pragma unroll
+                for (int t = 0; t < DH / 32; ++t) {
+                    const int c0 = 32 * t + 16 * (gg & 1) + 4 * gp;       // column of this lane's 8 bytes
+                    const int ch = c0 >> 3;
+                    const int rowa = r0, rowb = r0 + 8;
+                    const h16x4 lo = lds_read_tr16(Vl + rowa * RB +
+                                                   ((ch ^ ((((rowa >> 1) & 1) << 2) & (CH - 1))) << 4) + (c0 & 7) * 2);
+                    const h16x4 up = lds_read_tr16(Vl + rowb * RB +
+                                                   ((ch ^ ((((rowb >> 1) & 1) << 2) & (CH - 1))) << 4) + (c0 & 7) * 2);
+                    const h16x8 a = {lo[0], lo[1], lo[2], lo[3], up[0], up[1], up[2], up[3]};
+                    o[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bp, o[t], 0, 0, 0);
+                }
+            }
+        }
+    }
+
+    if (q < len) {
+        const float inv = 1.0f / l_i;
+        h16 *orow = out + (size_t)(start + q) * d + h * DH;
+#pragma unroll
+        for (int t = 0; t < DH / 32; ++t)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                h16x4 v;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = (h16)(o[t][4 * g + e] * inv);
+                *(h16x4 *)(orow + 32 * t + 8 * g + 4 * hi) = v;
+            }
+    }
+}
+
 void launch_attention(const uint16_t *qkv, const int32_t *cu, int32_t n_seqs, int32_t max_len, int32_t n_head,
                       int32_t d, uint16_t *out, hipStream_t s)
 {
     const int dh = d / n_head;
     const float sl2 = (1.0f / sqrtf((float)dh)) * 1.4426950408889634f;
+    if (max_len <= ATT_LDS_MAX && (dh == 64 || dh == 32)) {
+        if (dh == 64)
+            attention_lds_kernel<64><<<n_seqs * n_head, 1024, 0, s>>>((const h16 *)qkv, cu, d, n_head, sl2, (h16 *)out);
+        else
+            attention_lds_kernel<32><<<n_seqs * n_head, 1024, 0, s>>>((const h16 *)qkv, cu, d, n_head, sl2, (h16 *)out);
+        return;
+    }
     const int nqt = (max_len + ATT_QT - 1) / ATT_QT;
     const int grid = nqt * n_head * n_seqs;
     if (dh == 64)

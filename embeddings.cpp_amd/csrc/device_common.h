@@ -45,6 +45,16 @@ __device__ __forceinline__ void glds(const void *g, void *lds_base)
     else __builtin_amdgcn_global_load_lds(g, (lds_void_t *)lds_base, 4, 0, 0);
 }
 
+// ds_read_b64_tr_b16: per 16-lane group, a 4-row x 16-column block of 16-bit
+// values delivered column-major (lane i: column i of the 4 rows).  `p` is this
+// lane's LDS byte address (lane 4q+p of the group: row q, columns 4p..4p+3).
+typedef __fp16 fp16x4_tr __attribute__((vector_size(8)));
+__device__ __forceinline__ h16x4 lds_read_tr16(const void *p)
+{
+    const fp16x4_tr v = __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) fp16x4_tr *)p);
+    return __builtin_bit_cast(h16x4, v);
+}
+
 __device__ __forceinline__ void lds_barrier()
 {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

@@ -52,7 +52,8 @@ enum Epi : int32_t { EPI_BIAS_F16 = 0, EPI_BIAS_GELU_F16 = 1, EPI_BIAS_RES_F32 =
 
 constexpr int GEMM_BM = 256;          // token rows per tile (M is padded to this)
 constexpr int GEMM_BN = 128;          // output features per tile
-constexpr int ATT_QT = 128;           // queries per attention workgroup
+constexpr int ATT_QT = 128;           // queries per attention workgroup (sentences > ATT_LDS_MAX)
+constexpr int ATT_LDS_MAX = 512;      // sentences up to this length: whole K/V of a head in LDS
 
 // Deferred LayerNorm: the residual stream is kept PRE-LN (f32) with each row's
 // (mean, 1/sigma); a consumer that needs the normalised row recomputes it with
