@@ -169,6 +169,7 @@ Device::~Device()
 {
     (void)hipSetDevice(ordinal_);
     if (stream_) (void)hipStreamSynchronize(stream_);
+    drop_graphs();
     for (auto &p : pending_) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (auto e : free_events_) (void)hipEventDestroy(e);
     if (arena_) (void)hipFree(arena_);
@@ -286,6 +287,7 @@ bool Device::reserve(int64_t tokens, int64_t seqs)
     const size_t o_qkv = take(rows * 3 * d * 2), o_att = take(rows * d * 2), o_ffn = take(rows * f * 2);
     const size_t o_ids = take(rows * 4), o_cu = take((ns + 1) * 4), o_out = take(ns * d * 4);
     const size_t o_pool = take((size_t)ns * pool_chunks(hp_.n_max_tokens) * d * 4);
+    drop_graphs();   // captured graphs hold the old workspace pointers
     if (ws_) { (void)hipFree(ws_); ws_ = nullptr; }
     if (h_ids_) { (void)hipHostFree(h_ids_); h_ids_ = nullptr; }
     if (h_cu_) { (void)hipHostFree(h_cu_); h_cu_ = nullptr; }
@@ -356,19 +358,68 @@ void Device::reset_stats()
     for (auto &s : stats_) s = KStats();
 }
 
+void Device::drop_graphs()
+{
+    for (auto &g : graphs_) (void)hipGraphExecDestroy(g.exec);
+    graphs_.clear();
+    seen_once_.clear();
+}
+
 int Device::forward(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, int max_len, int T, float *d_out,
                     hipStream_t s)
 {
     if (!ok_) return -3;
     if (T > cap_tokens_ || n_seqs > cap_seqs_) return -2;
     if (T <= 0 || n_seqs <= 0) return 0;
+    // BERT_CHECK_FINITE=1: after every kernel, count non-finite outputs over the
+    // valid rows and report the first kernel that produced any (diagnostics).
+    static const bool check = [] { const char *e = std::getenv("BERT_CHECK_FINITE"); return e && *e == '1'; }();
+    static const bool graphs_env = [] { const char *e = std::getenv("BERT_GRAPHS"); return !(e && *e == '0'); }();
+    if (profiling_ || check || !use_graphs_ || !graphs_env || s == nullptr)
+        return launch_all(d_ids, d_cu, n_seqs, max_len, T, d_out, s, check);
+    const GraphKey key{d_ids, d_cu, d_out, s, n_seqs, max_len, T};
+    for (auto &g : graphs_)
+        if (g.key == key) return hipGraphLaunch(g.exec, s) == hipSuccess ? 0 : -1;
+    // a shape seen for the first time runs eagerly (one-off batches never pay
+    // for a capture); on its second use the sequence is captured and replayed
+    bool seen = false;
+    for (auto &k : seen_once_) seen = seen || (k == key);
+    if (!seen) {
+        if (seen_once_.size() >= 32) seen_once_.erase(seen_once_.begin());
+        seen_once_.push_back(key);
+        return launch_all(d_ids, d_cu, n_seqs, max_len, T, d_out, s, false);
+    }
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+        (void)hipGetLastError();
+        use_graphs_ = false;   // this runtime / stream cannot capture: stay eager
+        return launch_all(d_ids, d_cu, n_seqs, max_len, T, d_out, s, false);
+    }
+    const int rc = launch_all(d_ids, d_cu, n_seqs, max_len, T, d_out, s, false);
+    const hipError_t ec = hipStreamEndCapture(s, &graph);
+    if (rc != 0 || ec != hipSuccess || hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        if (graph) (void)hipGraphDestroy(graph);
+        use_graphs_ = false;
+        return launch_all(d_ids, d_cu, n_seqs, max_len, T, d_out, s, false);
+    }
+    (void)hipGraphDestroy(graph);
+    if (graphs_.size() >= 8) {
+        (void)hipGraphExecDestroy(graphs_.front().exec);
+        graphs_.erase(graphs_.begin());
+    }
+    graphs_.push_back({key, exec});
+    return hipGraphLaunch(exec, s) == hipSuccess ? 0 : -1;
+}
+
+int Device::launch_all(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, int max_len, int T, float *d_out,
+                       hipStream_t s, bool check)
+{
     const int d = hp_.n_embd, f = hp_.n_intermediate;
     const int M = (int)align_up((size_t)T, GEMM_BM);
     const double t = (double)T;
     hipEvent_t ev;
-    // BERT_CHECK_FINITE=1: after every kernel, count non-finite outputs over the
-    // valid rows and report the first kernel that produced any (diagnostics).
-    static const bool check = [] { const char *e = std::getenv("BERT_CHECK_FINITE"); return e && *e == '1'; }();
     unsigned *cnt = nullptr;
     bool bad = false;
     if (check) (void)hipMalloc((void **)&cnt, sizeof(unsigned));

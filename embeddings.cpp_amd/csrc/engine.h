@@ -45,7 +45,9 @@ public:
     // sentences fits (never called inside a timed forward).
     bool reserve(int64_t tokens, int64_t seqs);
 
-    // Device-resident forward (ids, cu, out on this GPU); async on `s`.
+    // Device-resident forward (ids, cu, out on this GPU); async on `s`.  When
+    // profiling is off and `s` is not the null stream, the launch sequence is
+    // captured once per (pointers, shape, stream) into a HIP graph and replayed.
     int forward(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, int max_len, int total_tokens, float *d_out,
                 hipStream_t s);
 
@@ -63,6 +65,20 @@ public:
 
 private:
     struct PendingEv { int cls; hipEvent_t a, b; double work; };
+    struct GraphKey {
+        const void *ids, *cu, *out;
+        hipStream_t s;
+        int n_seqs, max_len, T;
+        bool operator==(const GraphKey &o) const
+        {
+            return ids == o.ids && cu == o.cu && out == o.out && s == o.s && n_seqs == o.n_seqs &&
+                   max_len == o.max_len && T == o.T;
+        }
+    };
+    struct GraphEntry { GraphKey key; hipGraphExec_t exec; };
+    int launch_all(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, int max_len, int T, float *d_out,
+                   hipStream_t s, bool check);
+    void drop_graphs();
     void upload(const HostModel &m);
     void *arena_alloc(size_t bytes);
     void begin(int cls, hipStream_t s, hipEvent_t &a);
@@ -94,6 +110,11 @@ private:
     float *pool_part_ = nullptr;
     int32_t *h_ids_ = nullptr, *h_cu_ = nullptr;   // pinned staging
     float *h_out_ = nullptr;
+
+    // HIP graphs of the launch sequence (cleared when the workspace moves)
+    std::vector<GraphEntry> graphs_;
+    std::vector<GraphKey> seen_once_;   // a shape is captured on its second use
+    bool use_graphs_ = true;
 
     // profiling
     bool profiling_ = false;
