@@ -426,7 +426,7 @@ void dispatch_qw(const DevWeight &W, const h16 *x, int M, const float *bias, int
 // X: 2-stage LDS-DMA ring (64 KiB at BM 256), one K-step ahead; W: 3-set
 // register ring, two K-steps ahead; one barrier per K-step.
 // ---------------------------------------------------------------------------
-template <int FMT, int EPI, int BM>
+template <int FMT, int EPI, int BM, int NS>
 __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemmqv_kernel(DevWeight W, const h16 *__restrict__ X,
                                                         const float *__restrict__ bias, const float *__restrict__ res,
                                                         void *__restrict__ out, int nN, int nTiles, ResLN rln)
@@ -437,7 +437,9 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     constexpr int XG = XB / (256 * 16);        // LDS-DMA instructions per wave per stage
     constexpr int QB = qrec_bytes<FMT>();
     constexpr int LQ = QRegs<FMT>::LOADS;
-    __shared__ __attribute__((aligned(16))) char smem[2 * XB];
+    constexpr int P = LQ + XG;                  // ops issued per K-step per wave
+    static_assert(NS >= 2 && NS <= 4, "X ring depth");
+    __shared__ __attribute__((aligned(16))) char smem[NS * XB];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int b = blockIdx.x, xcd = b & 7, qq = nTiles >> 3, rr = nTiles & 7;
@@ -471,13 +473,29 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
 
-    // prologue: W(0), X(0) -> stage 0, W(1); retire W(0) and X(0)
+    // prologue: W(0), X(0) in flight first, then what the loop expects to be
+    // in flight at the end of step -1; retire W(0) and X(0)
     QRegs<FMT> w0, w1, w2;
     const int k1 = min(1, KS - 1);
     w0.load(wq, wd, wmn);
     EMB_ISSUE_XV(0, 0)
-    w1.load(wq + k1 * qstep, wd + k1 * sstep, FMT == FMT_Q4_1 ? wmn + k1 * sstep : nullptr);
-    wait_vmcnt<LQ>();
+    if constexpr (NS == 2) {               // order X, W: W(1)
+        w1.load(wq + k1 * qstep, wd + k1 * sstep, FMT == FMT_Q4_1 ? wmn + k1 * sstep : nullptr);
+        wait_vmcnt<LQ>();
+    } else if constexpr (NS == 3) {        // order W, X: [W(1), X(1)]
+        asm volatile("" ::: "memory");
+        w1.load(wq + k1 * qstep, wd + k1 * sstep, FMT == FMT_Q4_1 ? wmn + k1 * sstep : nullptr);
+        asm volatile("" ::: "memory");
+        EMB_ISSUE_XV(k1, 1)
+        wait_vmcnt<P>();
+    } else {                               // X(1), [W(1), X(2)]
+        EMB_ISSUE_XV(k1, 1)
+        asm volatile("" ::: "memory");
+        w1.load(wq + k1 * qstep, wd + k1 * sstep, FMT == FMT_Q4_1 ? wmn + k1 * sstep : nullptr);
+        asm volatile("" ::: "memory");
+        EMB_ISSUE_XV(min(2, KS - 1), 2)
+        wait_vmcnt<P + XG>();
+    }
     lds_barrier();
 
     const int sw = (lr >> 1) & 7;
@@ -491,32 +509,55 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     {                                                                                                     \
         const int ksx = (ks_);                                                                            \
         {                                                                                                 \
-            const int kx = min(ksx + 1, KS - 1), k2 = min(ksx + 2, KS - 1);                               \
-            EMB_ISSUE_XV(kx, st ^ 1)                                                                      \
-            asm volatile("" ::: "memory"); /* keep X(ks+1) older than W(ks+2): the end wait splits them */ \
-            NXT2.load(wq + k2 * qstep, wd + k2 * sstep, FMT == FMT_Q4_1 ? wmn + k2 * sstep : nullptr);    \
-            wait_vmcnt<2 * LQ + XG>();                                                                    \
+            const int kx = min(ksx + NS - 1, KS - 1), k2 = min(ksx + 2, KS - 1);                          \
+            const int sx = st == 0 ? NS - 1 : st - 1;   /* stage of X(ks + NS - 1) */                      \
+            if constexpr (NS == 2) {                                                                      \
+                EMB_ISSUE_XV(kx, sx)                                                                      \
+                asm volatile("" ::: "memory"); /* keep X(ks+1) older than W(ks+2): the end wait splits them */ \
+                NXT2.load(wq + k2 * qstep, wd + k2 * sstep, FMT == FMT_Q4_1 ? wmn + k2 * sstep : nullptr); \
+                wait_vmcnt<2 * LQ + XG>();                                                                \
+            } else {                                                                                      \
+                NXT2.load(wq + k2 * qstep, wd + k2 * sstep, FMT == FMT_Q4_1 ? wmn + k2 * sstep : nullptr); \
+                asm volatile("" ::: "memory"); /* W older than X: the end wait splits them */             \
+                EMB_ISSUE_XV(kx, sx)                                                                      \
+                wait_vmcnt<2 * P + (NS == 4 ? XG : 0)>();                                                 \
+            }                                                                                             \
             CUR.pin_all();                                                                                \
         }                                                                                                 \
         const char *xs = smem + st * XB + rbase;                                                          \
-        h16x8 bf[NJ], bn[NJ];                                                                             \
-        _Pragma("unroll") for (int j = 0; j < NJ; ++j) bf[j] = *(const h16x8 *)(xs + (j << 12) + (hi ^ sw) * 16); \
-        _Pragma("unroll") for (int kk = 0; kk < 4; ++kk)                                                  \
-        {                                                                                                 \
-            if (kk < 3) {                                                                                 \
-                const int cx = ((2 * kk + 2 + hi) ^ sw) << 4;                                             \
-                _Pragma("unroll") for (int j = 0; j < NJ; ++j) bn[j] = *(const h16x8 *)(xs + (j << 12) + cx); \
+        if constexpr (NJ <= 4) {  /* B fragments double-buffered across k-slices */                       \
+            h16x8 bf[NJ], bn[NJ];                                                                         \
+            _Pragma("unroll") for (int j = 0; j < NJ; ++j) bf[j] = *(const h16x8 *)(xs + (j << 12) + (hi ^ sw) * 16); \
+            _Pragma("unroll") for (int kk = 0; kk < 4; ++kk)                                              \
+            {                                                                                             \
+                if (kk < 3) {                                                                             \
+                    const int cx = ((2 * kk + 2 + hi) ^ sw) << 4;                                         \
+                    _Pragma("unroll") for (int j = 0; j < NJ; ++j) bn[j] = *(const h16x8 *)(xs + (j << 12) + cx); \
+                }                                                                                         \
+                const h16x8 a = CUR.frag(kk);                                                             \
+                _Pragma("unroll") for (int j = 0; j < NJ; ++j) acc[j] =                                   \
+                    __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bf[j], acc[j], 0, 0, 0);                    \
+                if (kk < 3) {                                                                             \
+                    _Pragma("unroll") for (int j = 0; j < NJ; ++j) bf[j] = bn[j];                         \
+                }                                                                                         \
             }                                                                                             \
-            const h16x8 a = CUR.frag(kk);                                                                 \
-            _Pragma("unroll") for (int j = 0; j < NJ; ++j) acc[j] =                                       \
-                __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bf[j], acc[j], 0, 0, 0);                        \
-            if (kk < 3) {                                                                                 \
-                _Pragma("unroll") for (int j = 0; j < NJ; ++j) bf[j] = bn[j];                             \
+        } else {                  /* NJ = 8: registers are tight (acc alone is 128) */                     \
+            _Pragma("unroll") for (int kk = 0; kk < 4; ++kk)                                              \
+            {                                                                                             \
+                const int cx = ((2 * kk + hi) ^ sw) << 4;                                                 \
+                h16x8 bf[NJ];                                                                             \
+                _Pragma("unroll") for (int j = 0; j < NJ; ++j) bf[j] = *(const h16x8 *)(xs + (j << 12) + cx); \
+                const h16x8 a = CUR.frag(kk);                                                             \
+                _Pragma("unroll") for (int j = 0; j < NJ; ++j) acc[j] =                                   \
+                    __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bf[j], acc[j], 0, 0, 0);                    \
             }                                                                                             \
         }                                                                                                 \
-        wait_vmcnt<LQ>(); /* X(ks+1), W(ks+1) landed; W(ks+2) may fly */                                 \
+        /* X(ks+1), W(ks+1) landed; younger issues may fly */                                          \
+        if constexpr (NS == 2) wait_vmcnt<LQ>();                                                          \
+        else if constexpr (NS == 3) wait_vmcnt<P>();                                                      \
+        else wait_vmcnt<P + XG>();                                                                        \
         lds_barrier();                                                                                    \
-        st ^= 1;                                                                                          \
+        st = st == NS - 1 ? 0 : st + 1;                                                                   \
     }
 
     int ks = 0;
@@ -609,13 +650,15 @@ template <int FMT, int BM>
 void dispatch_qv(const DevWeight &W, const h16 *x, int M, const float *bias, int epi, const float *res, void *out,
                  hipStream_t s, const ResLN &rln)
 {
+    // X ring: 2 stages of 32 KiB at BM 256, 4 of 16 KiB at BM 128 (64 KiB per workgroup)
+    constexpr int NS = BM == 256 ? 2 : 4;
     const int nN = (W.N + 127) / 128, nTiles = (M / BM) * nN;
     if (epi == EPI_BIAS_F16)
-        gemmqv_kernel<FMT, EPI_BIAS_F16, BM><<<nTiles, 256, 0, s>>>(W, x, bias, res, out, nN, nTiles, rln);
+        gemmqv_kernel<FMT, EPI_BIAS_F16, BM, NS><<<nTiles, 256, 0, s>>>(W, x, bias, res, out, nN, nTiles, rln);
     else if (epi == EPI_BIAS_GELU_F16)
-        gemmqv_kernel<FMT, EPI_BIAS_GELU_F16, BM><<<nTiles, 256, 0, s>>>(W, x, bias, res, out, nN, nTiles, rln);
+        gemmqv_kernel<FMT, EPI_BIAS_GELU_F16, BM, NS><<<nTiles, 256, 0, s>>>(W, x, bias, res, out, nN, nTiles, rln);
     else
-        gemmqv_kernel<FMT, EPI_BIAS_RES_F32, BM><<<nTiles, 256, 0, s>>>(W, x, bias, res, out, nN, nTiles, rln);
+        gemmqv_kernel<FMT, EPI_BIAS_RES_F32, BM, NS><<<nTiles, 256, 0, s>>>(W, x, bias, res, out, nN, nTiles, rln);
 }
 
 }  // namespace
