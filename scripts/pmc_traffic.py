@@ -37,7 +37,7 @@ def classify(rows):
     out, res_i = [], 0
     for r in rows:
         k = r["Kernel_Name"]
-        m = re.search(r"gemm(?:q)?_kernelILi(\d+)ELi(\d+)E", k)
+        m = re.search(r"gemmq[vw]?_kernelILi(\d+)ELi(\d+)E", k)
         if m:
             epi = int(m.group(2))
             if epi == 0:
