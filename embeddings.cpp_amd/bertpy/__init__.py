@@ -71,7 +71,7 @@ def load_lib(path=None):
     L.bertx_quantize_file.restype = c_i32
     L.bertx_quantize_file.argtypes = [ctypes.c_char_p, ctypes.c_char_p, c_i32]
     L.bertx_test_gemm.restype = c_i32
-    L.bertx_test_gemm.argtypes = [c_i32, c_i32, c_i32, vp, c_f32p, c_i32, vp, c_i32, c_f32p, vp, c_i32]
+    L.bertx_test_gemm.argtypes = [c_i32, c_i32, c_i32, vp, c_f32p, c_i32, vp, c_i32, vp, vp, c_i32]
     L.bertx_bench_gemm.restype = c_i32
     L.bertx_bench_gemm.argtypes = [c_i32] * 8 + [c_f32p]
     L.bertx_version.restype = ctypes.c_char_p

@@ -102,7 +102,7 @@ private:
     // workspace
     int64_t cap_tokens_ = 0, cap_seqs_ = 0;
     char *ws_ = nullptr;
-    float *y32_ = nullptr;          // pre-LN residual stream
+    uint16_t *yh_ = nullptr;        // pre-LN residual stream (f16)
     float2 *st_ = nullptr;          // (mean, 1/sigma) of its last LN
     uint16_t *xh_ = nullptr, *qkv_ = nullptr, *att_ = nullptr, *ffn_ = nullptr;
     int32_t *d_ids_ = nullptr, *d_cu_ = nullptr;

@@ -170,7 +170,7 @@ constexpr int qrec_bytes() { return FMT == FMT_F16 ? 128 : FMT == FMT_Q8_0 ? 64 
 // in the K loop, 0x8 no MFMA.
 template <int FMT, int EPI, int WM, int DIAG = 0>
 __global__ __launch_bounds__(512, 1) void gemmqw_kernel(DevWeight W, const h16 *__restrict__ X,
-                                                        const float *__restrict__ bias, const float *__restrict__ res,
+                                                        const float *__restrict__ bias, const void *__restrict__ res,
                                                         void *__restrict__ out, int nN, int nTiles, ResLN rln,
                                                         uint64_t *__restrict__ stamps = nullptr)
 {
@@ -235,6 +235,9 @@ __global__ __launch_bounds__(512, 1) void gemmqw_kernel(DevWeight W, const h16 *
     const int sw = (lr >> 1) & 7;
     const int rbase = (wm * TM + lr) << 7;
     int st = 0;
+    if constexpr (DIAG & 0x80) {   // static priority for the younger half (waves 4-7)
+        if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+    }
     h16x8 bdiag[(DIAG & 0x2) ? NJ : 1];
     if constexpr (DIAG & 0x2) {
 #pragma unroll
@@ -297,8 +300,10 @@ __global__ __launch_bounds__(512, 1) void gemmqw_kernel(DevWeight W, const h16 *
             if constexpr (DIAG & 0x8) {                                                                   \
                 _Pragma("unroll") for (int j = 0; j < NJ; ++j) asm volatile("" :: "v"(a), "v"(bf[j]));   \
             } else {                                                                                      \
+                if constexpr (DIAG & 0x40) __builtin_amdgcn_s_setprio(1);                                 \
                 _Pragma("unroll") for (int j = 0; j < NJ; ++j) acc[j] =                                   \
                     __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bf[j], acc[j], 0, 0, 0);                    \
+                if constexpr (DIAG & 0x40) __builtin_amdgcn_s_setprio(0);                                 \
             }                                                                                             \
         }                                                                                                 \
         wait_vmcnt<P>(); /* step ks+1's W and X landed; step ks+2's may fly */                           \
@@ -331,7 +336,7 @@ __global__ __launch_bounds__(512, 1) void gemmqw_kernel(DevWeight W, const h16 *
     f32x4 bb[4];
 #pragma unroll
     for (int g = 0; g < 4; ++g) bb[g] = *(const f32x4 *)(bias + nw + 8 * g + 4 * hi);
-    if constexpr (EPI == EPI_BIAS_RES_F32) {
+    if constexpr (EPI == EPI_BIAS_RES) {
         f32x4 lw[4], lb[4];
         if (rln.stats) {
 #pragma unroll
@@ -345,7 +350,10 @@ __global__ __launch_bounds__(512, 1) void gemmqw_kernel(DevWeight W, const h16 *
             const size_t rowo = (size_t)(mrow + 32 * j) * N + nw + 4 * hi;
             f32x4 rv[4];
 #pragma unroll
-            for (int g = 0; g < 4; ++g) rv[g] = *(const f32x4 *)(res + rowo + 8 * g);
+            for (int g = 0; g < 4; ++g) {
+                const h16x4 r4 = *(const h16x4 *)((const h16 *)res + rowo + 8 * g);
+                rv[g] = f32x4{(float)r4[0], (float)r4[1], (float)r4[2], (float)r4[3]};
+            }
             if (rln.stats) {                   // residual = LN(pre-LN row), recomputed
                 const float2 st = rln.stats[mrow + 32 * j];
 #pragma unroll
@@ -355,10 +363,10 @@ __global__ __launch_bounds__(512, 1) void gemmqw_kernel(DevWeight W, const h16 *
             }
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                f32x4 o;
+                h16x4 o;
 #pragma unroll
-                for (int e = 0; e < 4; ++e) o[e] = rv[g][e] + (bb[g][e] + acc[j][4 * g + e]);
-                *(f32x4 *)((float *)out + rowo + 8 * g) = o;
+                for (int e = 0; e < 4; ++e) o[e] = (h16)(rv[g][e] + (bb[g][e] + acc[j][4 * g + e]));
+                *(h16x4 *)((h16 *)out + rowo + 8 * g) = o;
             }
         }
     } else {
@@ -401,7 +409,7 @@ __global__ __launch_bounds__(512, 1) void gemmqw_kernel(DevWeight W, const h16 *
 }
 
 template <int FMT, int WM, int STAMP = 0>
-void dispatch_qw(const DevWeight &W, const h16 *x, int M, const float *bias, int epi, const float *res, void *out,
+void dispatch_qw(const DevWeight &W, const h16 *x, int M, const float *bias, int epi, const void *res, void *out,
                  hipStream_t s, const ResLN &rln, uint64_t *stamps = nullptr)
 {
     constexpr int BN = 256 / WM;
@@ -412,7 +420,7 @@ void dispatch_qw(const DevWeight &W, const h16 *x, int M, const float *bias, int
         gemmqw_kernel<FMT, EPI_BIAS_GELU_F16, WM, STAMP><<<nTiles, 512, 0, s>>>(W, x, bias, res, out, nN, nTiles, rln,
                                                                               stamps);
     else
-        gemmqw_kernel<FMT, EPI_BIAS_RES_F32, WM, STAMP><<<nTiles, 512, 0, s>>>(W, x, bias, res, out, nN, nTiles, rln,
+        gemmqw_kernel<FMT, EPI_BIAS_RES, WM, STAMP><<<nTiles, 512, 0, s>>>(W, x, bias, res, out, nN, nTiles, rln,
                                                                              stamps);
 }
 
@@ -428,7 +436,7 @@ void dispatch_qw(const DevWeight &W, const h16 *x, int M, const float *bias, int
 // ---------------------------------------------------------------------------
 template <int FMT, int EPI, int BM, int NS>
 __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemmqv_kernel(DevWeight W, const h16 *__restrict__ X,
-                                                        const float *__restrict__ bias, const float *__restrict__ res,
+                                                        const float *__restrict__ bias, const void *__restrict__ res,
                                                         void *__restrict__ out, int nN, int nTiles, ResLN rln)
 {
     constexpr int BN = 128;
@@ -580,13 +588,15 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     f32x4 bb[4];
 #pragma unroll
     for (int g = 0; g < 4; ++g) bb[g] = *(const f32x4 *)(bias + nw + 8 * g + 4 * hi);
-    if constexpr (EPI == EPI_BIAS_RES_F32) {
+    if constexpr (EPI == EPI_BIAS_RES) {
         f32x4 rv[NJ][4];                       // all residual loads in flight at once
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
 #pragma unroll
-            for (int g = 0; g < 4; ++g)
-                rv[j][g] = *(const f32x4 *)(res + (size_t)(mrow + 32 * j) * N + nw + 4 * hi + 8 * g);
+            for (int g = 0; g < 4; ++g) {
+                const h16x4 r4 = *(const h16x4 *)((const h16 *)res + (size_t)(mrow + 32 * j) * N + nw + 4 * hi + 8 * g);
+                rv[j][g] = f32x4{(float)r4[0], (float)r4[1], (float)r4[2], (float)r4[3]};
+            }
         if (rln.stats) {                       // residual = LN(pre-LN row), recomputed
             f32x4 lw[4], lb[4];
 #pragma unroll
@@ -608,10 +618,10 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             const size_t rowo = (size_t)(mrow + 32 * j) * N + nw + 4 * hi;
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                f32x4 o;
+                h16x4 o;
 #pragma unroll
-                for (int e = 0; e < 4; ++e) o[e] = rv[j][g][e] + (bb[g][e] + acc[j][4 * g + e]);
-                *(f32x4 *)((float *)out + rowo + 8 * g) = o;
+                for (int e = 0; e < 4; ++e) o[e] = (h16)(rv[j][g][e] + (bb[g][e] + acc[j][4 * g + e]));
+                *(h16x4 *)((h16 *)out + rowo + 8 * g) = o;
             }
         }
     } else {
@@ -647,7 +657,7 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 }
 
 template <int FMT, int BM>
-void dispatch_qv(const DevWeight &W, const h16 *x, int M, const float *bias, int epi, const float *res, void *out,
+void dispatch_qv(const DevWeight &W, const h16 *x, int M, const float *bias, int epi, const void *res, void *out,
                  hipStream_t s, const ResLN &rln)
 {
     // X ring: 2 stages of 32 KiB at BM 256, 4 of 16 KiB at BM 128 (64 KiB per workgroup)
@@ -658,7 +668,7 @@ void dispatch_qv(const DevWeight &W, const h16 *x, int M, const float *bias, int
     else if (epi == EPI_BIAS_GELU_F16)
         gemmqv_kernel<FMT, EPI_BIAS_GELU_F16, BM, NS><<<nTiles, 256, 0, s>>>(W, x, bias, res, out, nN, nTiles, rln);
     else
-        gemmqv_kernel<FMT, EPI_BIAS_RES_F32, BM, NS><<<nTiles, 256, 0, s>>>(W, x, bias, res, out, nN, nTiles, rln);
+        gemmqv_kernel<FMT, EPI_BIAS_RES, BM, NS><<<nTiles, 256, 0, s>>>(W, x, bias, res, out, nN, nTiles, rln);
 }
 
 }  // namespace
@@ -666,7 +676,7 @@ void dispatch_qv(const DevWeight &W, const h16 *x, int M, const float *bias, int
 // Diagnostics: q4_0 gemmqw with per-wave s_memtime stamps (4 per wave) into `stamps`
 // (device buffer of nTiles * 8 * 4 uint64).  Returns the tile count.
 int launch_gemm_q_stamped(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi,
-                          const float *res, void *out, hipStream_t s, int32_t wm, uint64_t *stamps, int32_t diag)
+                          const void *res, void *out, hipStream_t s, int32_t wm, uint64_t *stamps, int32_t diag)
 {
     const h16 *x = (const h16 *)X;
     const int BN = 256 / wm;
@@ -680,6 +690,9 @@ int launch_gemm_q_stamped(const DevWeight &W, const uint16_t *X, int32_t M, cons
         case 15: dispatch_qw<FMT_Q4_0, 1, 0x1f>(W, x, M, bias, epi, res, out, s, ResLN(), stamps); break;
         case 32: dispatch_qw<FMT_Q4_0, 1, 0x30>(W, x, M, bias, epi, res, out, s, ResLN(), stamps); break;
         case 36: dispatch_qw<FMT_Q4_0, 1, 0x34>(W, x, M, bias, epi, res, out, s, ResLN(), stamps); break;
+        case 64: dispatch_qw<FMT_Q4_0, 1, 0x50>(W, x, M, bias, epi, res, out, s, ResLN(), stamps); break;
+        case 128: dispatch_qw<FMT_Q4_0, 1, 0x90>(W, x, M, bias, epi, res, out, s, ResLN(), stamps); break;
+        case 192: dispatch_qw<FMT_Q4_0, 1, 0xd0>(W, x, M, bias, epi, res, out, s, ResLN(), stamps); break;
         default: dispatch_qw<FMT_Q4_0, 1, 0x10>(W, x, M, bias, epi, res, out, s, ResLN(), stamps); break;
         }
     } else {
@@ -692,7 +705,7 @@ int g_gemm_variant = 0;   // 0: heuristic (gemmqv, gemmqw for the GELU form), 2:
 int g_force_bn = 0;       // tests: force the tile shape (128 / 256; 0 = heuristic)
 
 template <int FMT>
-void launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, int32_t epi, const float *res,
+void launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, int32_t epi, const void *res,
                 void *out, hipStream_t s, const ResLN &rln)
 {
     const int force = g_force_bn;
@@ -709,12 +722,12 @@ void launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, 
         return;
     }
     // 2 workgroups / CU; BM 128 for the residual (f32) form and for small M
-    const bool big = force ? force == 256 : (epi != EPI_BIAS_RES_F32 && M >= 256 * 64);
+    const bool big = force ? force == 256 : (epi != EPI_BIAS_RES && M >= 256 * 64);
     if (big) dispatch_qv<FMT, 256>(W, x, M, bias, epi, res, out, s, rln);
     else dispatch_qv<FMT, 128>(W, x, M, bias, epi, res, out, s, rln);
 }
 
-void launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi, const float *res,
+void launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi, const void *res,
                  void *out, hipStream_t s, const ResLN &rln)
 {
     const h16 *x = (const h16 *)X;

@@ -21,7 +21,7 @@
 //   tables   word/type/pos embeddings in the file's format; q blocks split
 //            into an aligned 16/32 B plane + f16 d (+ m) planes.
 // Activations (per device workspace, rows = packed tokens of all sentences):
-//   Y32 [T][d] f32 residual stream kept PRE-LayerNorm + ST [T] (mean, 1/sigma)
+//   YH [T][d] f16 residual stream kept PRE-LayerNorm + ST [T] (mean, 1/sigma)
 //   of its last LN (the normalised row is recomputed where it is consumed),
 //   XH [T][d] f16 normalised copy (GEMM input), QKV [T][3d] f16, ATT [T][d] f16,
 //   FFN [T][f] f16.
@@ -48,7 +48,7 @@ struct DevTable {
     const uint16_t *m = nullptr;
 };
 
-enum Epi : int32_t { EPI_BIAS_F16 = 0, EPI_BIAS_GELU_F16 = 1, EPI_BIAS_RES_F32 = 2 };
+enum Epi : int32_t { EPI_BIAS_F16 = 0, EPI_BIAS_GELU_F16 = 1, EPI_BIAS_RES = 2 };
 
 constexpr int GEMM_BM = 256;          // token rows per tile (M is padded to this)
 constexpr int GEMM_BN = 128;          // output features per tile
@@ -68,10 +68,11 @@ __host__ __device__ __forceinline__ float ln_apply(float v, float mean, float sc
 }
 
 // Y[m][n] = epi( sum_k X[m][k] W[n][k] ), X f16 [M][K] with M % GEMM_BM == 0.
-// EPI_BIAS_RES_F32: Y = LN(res) + acc + bias with LN given by `rln` (identity if
-// rln.stats is null); res may alias out (in place, element-wise).
+// EPI_BIAS_RES: Y = LN(res) + acc + bias (f32 math; res and Y f16, the residual
+// stream) with LN given by `rln` (identity if rln.stats is null); res may alias
+// out (in place, element-wise).
 void launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi,
-                 const float *res, void *out, hipStream_t s, const ResLN &rln = ResLN());
+                 const void *res, void *out, hipStream_t s, const ResLN &rln = ResLN());
 
 // Tests only: force the GEMM tile shape (128 / 256; 0 = heuristic).
 extern int g_force_bn;
@@ -79,29 +80,29 @@ extern int g_force_bn;
 extern int g_gemm_variant;
 // Diagnostics: q4_0 gemmqw (wm waves along tokens) with per-wave s_memtime stamps.
 int launch_gemm_q_stamped(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi,
-                          const float *res, void *out, hipStream_t s, int32_t wm, uint64_t *stamps,
+                          const void *res, void *out, hipStream_t s, int32_t wm, uint64_t *stamps,
                           int32_t diag);
 
-// y32 = pos[i] + (type[0] + word[id]) (pre-LN), xh = f16(LN(y32)), stats, for
+// yh = f16(pos[i] + (type[0] + word[id])) (pre-LN), xh = f16(LN(yh)), stats, for
 // every valid token (bert.cpp:963-984).
 void launch_embed_ln(const DevTable &word, const DevTable &type, const DevTable &pos, const float *ln_w,
                      const float *ln_b, const int32_t *ids, const int32_t *cu, int32_t n_seqs, int32_t max_len,
-                     int32_t d, float *y32, uint16_t *xh, float2 *stats, hipStream_t s);
+                     int32_t d, uint16_t *yh, uint16_t *xh, float2 *stats, hipStream_t s);
 
-// xh = f16(LN(y)), stats = (mean, 1/sigma) per row, for T rows.
-void launch_layernorm(const float *y, int32_t T, int32_t d, const float *w, const float *b, uint16_t *xh,
+// xh = f16(LN(yh)), stats = (mean, 1/sigma) per row, for T rows (yh f16).
+void launch_layernorm(const uint16_t *yh, int32_t T, int32_t d, const float *w, const float *b, uint16_t *xh,
                       float2 *stats, hipStream_t s);
 
 // Per (sentence, head) softmax(Q K^T / sqrt(dh)) V over the sentence's own keys.
 void launch_attention(const uint16_t *qkv, const int32_t *cu, int32_t n_seqs, int32_t max_len, int32_t n_head,
                       int32_t d, uint16_t *out, hipStream_t s);
 
-// out[b] = mean_{i<len} LN(y32[start+i]) / ||.||  (bert.cpp:1087-1095).
+// out[b] = mean_{i<len} LN(yh[start+i]) / ||.||  (bert.cpp:1087-1095).
 // Two stages: per-64-token-chunk partial sums into partial[n_seqs][pool_chunks][d],
 // then sum + normalise.
 int32_t pool_chunks(int32_t max_len);
-void launch_pool_l2(const float *y32, const ResLN &ln, const int32_t *cu, int32_t n_seqs, int32_t max_len, int32_t d,
-                    float *partial, float *out, hipStream_t s);
+void launch_pool_l2(const uint16_t *yh, const ResLN &ln, const int32_t *cu, int32_t n_seqs, int32_t max_len,
+                    int32_t d, float *partial, float *out, hipStream_t s);
 
 // Diagnostics: *cnt += number of non-finite values in p[0..n) (f32, or f16 if f16).
 void launch_count_nonfinite(const void *p, size_t n, int f16, unsigned *cnt, hipStream_t s);

@@ -90,7 +90,7 @@ __device__ __forceinline__ void ln_row(f32x4 (&v)[MAXV], int d, int lane, const 
 __global__ __launch_bounds__(256) void embed_ln_kernel(DevTable word, DevTable type, DevTable pos,
                                                        const float *__restrict__ ln_w, const float *__restrict__ ln_b,
                                                        const int32_t *__restrict__ ids, const int32_t *__restrict__ cu,
-                                                       int d, float *__restrict__ y32, h16 *__restrict__ xh,
+                                                       int d, h16 *__restrict__ yh, h16 *__restrict__ xh,
                                                        float2 *__restrict__ stats)
 {
     const int b = blockIdx.y, lane = threadIdx.x & 63;
@@ -105,15 +105,19 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(DevTable word, DevTable t
         if (c < d) {
             // pos + (type[0] + word[id])  (bert.cpp:968-973 operand order)
             const f32x4 w = table4(word, id, c), ty = table4(type, 0, c), p = table4(pos, i, c);
+            h16x4 v16;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[k][e] = p[e] + (ty[e] + w[e]);
-            *(f32x4 *)(y32 + (size_t)t * d + c) = v[k];          // pre-LN residual stream
+            for (int e = 0; e < 4; ++e) {
+                v16[e] = (h16)(p[e] + (ty[e] + w[e]));
+                v[k][e] = (float)v16[e];       // LN of the stored (f16) residual value
+            }
+            *(h16x4 *)(yh + (size_t)t * d + c) = v16;            // pre-LN residual stream
         }
     }
     ln_row(v, d, lane, ln_w, ln_b, xh + (size_t)t * d, stats + t);
 }
 
-__global__ __launch_bounds__(256) void layernorm_kernel(const float *__restrict__ y, int T, int d,
+__global__ __launch_bounds__(256) void layernorm_kernel(const h16 *__restrict__ y, int T, int d,
                                                         const float *__restrict__ w, const float *__restrict__ b,
                                                         h16 *__restrict__ xh, float2 *__restrict__ stats)
 {
@@ -121,11 +125,14 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float *__restrict_
     const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (t >= T) return;
     f32x4 v[MAXV];
-    const float *row = y + (size_t)t * d;
+    const h16 *row = y + (size_t)t * d;
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) {
         const int c = 4 * (lane + 64 * k);
-        if (c < d) v[k] = *(const f32x4 *)(row + c);
+        if (c < d) {
+            const h16x4 r = *(const h16x4 *)(row + c);
+            v[k] = f32x4{(float)r[0], (float)r[1], (float)r[2], (float)r[3]};
+        }
     }
     ln_row(v, d, lane, w, b, xh + (size_t)t * d, stats + t);
 }
@@ -134,7 +141,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float *__restrict_
 // (bert.cpp:1087-1089: sum_i X[i][c] * (1/len)).
 constexpr int POOL_CHUNK = 64;
 
-__global__ __launch_bounds__(256) void pool_partial_kernel(const float *__restrict__ y32, const float2 *__restrict__ stats,
+__global__ __launch_bounds__(256) void pool_partial_kernel(const h16 *__restrict__ y32, const float2 *__restrict__ stats,
                                                            const float *__restrict__ lw, const float *__restrict__ lb,
                                                            const int32_t *__restrict__ cu, int d, int n_chunks,
                                                            float *__restrict__ part)
@@ -149,10 +156,10 @@ __global__ __launch_bounds__(256) void pool_partial_kernel(const float *__restri
         const f32x4 ww = *(const f32x4 *)(lw + c), bb = *(const f32x4 *)(lb + c);
         const int i1 = min(len, i0 + POOL_CHUNK);
         for (int i = i0; i < i1; ++i) {
-            const f32x4 y = *(const f32x4 *)(y32 + (size_t)(start + i) * d + c);
+            const h16x4 y = *(const h16x4 *)(y32 + (size_t)(start + i) * d + c);
             const float2 st = stats[start + i];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) a[e] += ln_apply(y[e], st.x, st.y, ww[e], bb[e]) * wt;
+            for (int e = 0; e < 4; ++e) a[e] += ln_apply((float)y[e], st.x, st.y, ww[e], bb[e]) * wt;
         }
         *(f32x4 *)(dst + c) = a;
     }
@@ -201,25 +208,25 @@ void launch_count_nonfinite(const void *p, size_t n, int f16, unsigned *cnt, hip
 
 void launch_embed_ln(const DevTable &word, const DevTable &type, const DevTable &pos, const float *ln_w,
                      const float *ln_b, const int32_t *ids, const int32_t *cu, int32_t n_seqs, int32_t max_len,
-                     int32_t d, float *y32, uint16_t *xh, float2 *stats, hipStream_t s)
+                     int32_t d, uint16_t *yh, uint16_t *xh, float2 *stats, hipStream_t s)
 {
     dim3 grid((max_len + 3) / 4, n_seqs);
-    embed_ln_kernel<<<grid, 256, 0, s>>>(word, type, pos, ln_w, ln_b, ids, cu, d, y32, (h16 *)xh, stats);
+    embed_ln_kernel<<<grid, 256, 0, s>>>(word, type, pos, ln_w, ln_b, ids, cu, d, (h16 *)yh, (h16 *)xh, stats);
 }
 
-void launch_layernorm(const float *y, int32_t T, int32_t d, const float *w, const float *b, uint16_t *xh,
+void launch_layernorm(const uint16_t *yh, int32_t T, int32_t d, const float *w, const float *b, uint16_t *xh,
                       float2 *stats, hipStream_t s)
 {
-    layernorm_kernel<<<(T + 3) / 4, 256, 0, s>>>(y, T, d, w, b, (h16 *)xh, stats);
+    layernorm_kernel<<<(T + 3) / 4, 256, 0, s>>>((const h16 *)yh, T, d, w, b, (h16 *)xh, stats);
 }
 
 int32_t pool_chunks(int32_t max_len) { return (max_len + POOL_CHUNK - 1) / POOL_CHUNK; }
 
-void launch_pool_l2(const float *y32, const ResLN &ln, const int32_t *cu, int32_t n_seqs, int32_t max_len, int32_t d,
-                    float *partial, float *out, hipStream_t s)
+void launch_pool_l2(const uint16_t *yh, const ResLN &ln, const int32_t *cu, int32_t n_seqs, int32_t max_len,
+                    int32_t d, float *partial, float *out, hipStream_t s)
 {
     const int nc = pool_chunks(max_len);
-    pool_partial_kernel<<<dim3(nc, n_seqs), 256, 0, s>>>(y32, ln.stats, ln.w, ln.b, cu, d, nc, partial);
+    pool_partial_kernel<<<dim3(nc, n_seqs), 256, 0, s>>>((const h16 *)yh, ln.stats, ln.w, ln.b, cu, d, nc, partial);
     pool_final_kernel<<<n_seqs, 256, 0, s>>>(partial, d, nc, out);
 }
 

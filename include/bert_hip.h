@@ -62,12 +62,13 @@ BERT_API int32_t bertx_quantize_file(const char *fname_in, const char *fname_out
  * Per-kernel parity hooks (host buffers in/out, runs synchronously on the
  * first device).  w_rows: the weight exactly as the model file stores it
  * (N rows of K elements in format `fmt` = 0,1,2,3,8).  x: f16 bits [M][K].
- * epi: 0 = +bias -> f16, 1 = +bias, GELU -> f16, 2 = +bias +res(f32) -> f32.
+ * epi: 0 = +bias -> f16, 1 = +bias, GELU -> f16, 2 = +bias +res -> f16 (res f16 [M][N],
+ * the residual-stream form; sum in f32).
  * tile_n: 0 = the production tile choice, 128 / 256 = force that tile width.
  */
 BERT_API int32_t bertx_test_gemm(int32_t fmt, int32_t N, int32_t K, const void *w_rows,
                                  const float *bias, int32_t M, const uint16_t *x,
-                                 int32_t epi, const float *res, void *out, int32_t tile_n);
+                                 int32_t epi, const void *res, void *out, int32_t tile_n);
 
 /*
  * GEMM micro-benchmark on random operands (device 0): average device time of

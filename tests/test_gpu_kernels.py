@@ -38,11 +38,11 @@ def run_gemm(lib, fmt, W, bias, X, epi, res=None, tile_n=0):
     M = X.shape[0]
     wb, deq = weight_rows(fmt, W)
     xh = np.ascontiguousarray(X.astype(np.float16))
-    out = np.zeros((M, N), np.float32 if epi == 2 else np.float16)
+    out = np.zeros((M, N), np.float16)
     resp = None
-    if epi == 2:
-        res = np.ascontiguousarray(res, np.float32)
-        resp = res.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+    if epi == 2:                          # the residual stream is f16
+        res = np.ascontiguousarray(res, np.float16)
+        resp = res.ctypes.data
     rc = lib.bertx_test_gemm(fmt, N, K, wb, np.ascontiguousarray(bias, np.float32).ctypes.data_as(
         ctypes.POINTER(ctypes.c_float)), M, xh.ctypes.data, epi, resp, out.ctypes.data, tile_n)
     assert rc == 0
@@ -56,14 +56,14 @@ def run_gemm(lib, fmt, W, bias, X, epi, res=None, tile_n=0):
 def test_gemm_matches_numpy(lib, fmt, epi, shape):
     N, K, M, tile_n = shape
     if tile_n == 256 and epi == 2:
-        pytest.skip("the f32 residual epilogue only exists 128 wide")
+        pytest.skip("the residual epilogue runs 128 wide")
     rng = np.random.default_rng(fmt * 10 + epi)
     W = rng.standard_normal((N, K)).astype(np.float32) * 0.05
     W[:, 5] *= 20.0                       # asymmetric outliers catch transposed maps
     bias = rng.standard_normal(N).astype(np.float32) * 0.1
     X = rng.standard_normal((M, K)).astype(np.float32)
     X[7] *= 3.0
-    res = rng.standard_normal((M, N)).astype(np.float32) if epi == 2 else None
+    res = rng.standard_normal((M, N)).astype(np.float16) if epi == 2 else None
     got, deq, xh = run_gemm(lib, fmt, W, bias, X, epi, res, tile_n)
     # the kernel multiplies f16 operands with f32 accumulation: reference uses f16(weights)
     wref = deq.astype(np.float16).astype(np.float64)
@@ -75,9 +75,9 @@ def test_gemm_matches_numpy(lib, fmt, epi, shape):
         x16 = acc.astype(np.float16).astype(np.float64)
         ref = 0.5 * x16 * (1 + np.tanh(0.7978845608028654 * x16 * (1 + 0.044715 * x16 * x16)))
         tol = 3e-3 * np.abs(ref).max()
-    else:
+    else:                                 # f32 sum of the f16 residual, rounded to f16
         ref = res.astype(np.float64) + acc
-        tol = 2e-5 * np.abs(ref).max() * np.sqrt(K / 64)
+        tol = 2e-3 * np.abs(ref).max()
     err = np.abs(got - ref).max()
     assert err <= tol, (FMTS[fmt], epi, err, tol)
     # and the dequantized value itself is what the reference uses (f32 math)
