@@ -35,6 +35,24 @@ __device__ __forceinline__ h16 gelu_era(float v)
     return (h16)(x * __builtin_amdgcn_rcpf(1.0f + e));
 }
 
+// Two GELUs in packed f16 (the epilogue form): x = f16(v) as the era table's
+// input, then x * sigmoid(2u) with z = -2 log2(e) u evaluated in f16 pairs, one
+// f16 exp2 and one f16 rcp per element.  Within 10 f16 ulps of the table
+// (mean 0.5 ulp, |x| < 12); returns the two f16 results packed.
+__device__ __forceinline__ uint32_t gelu2_era(float a, float b)
+{
+    const h16x2 x = {(h16)a, (h16)b};
+    const h16 c0 = (h16)(-2.0f * 1.4426950408889634f * 0.7978845608028654f);
+    const h16 c1 = (h16)(-2.0f * 1.4426950408889634f * 0.7978845608028654f * 0.044715f);
+    const h16x2 C0 = {c0, c0}, C1 = {c1, c1}, ONE = {(h16)1.0f, (h16)1.0f};
+    const h16x2 z = x * (x * x * C1 + C0);
+    const h16x2 d = __builtin_elementwise_exp2(z) + ONE;
+    h16x2 r;
+    r.x = __builtin_amdgcn_rcph(d.x);
+    r.y = __builtin_amdgcn_rcph(d.y);
+    return __builtin_bit_cast(uint32_t, x * r);
+}
+
 // LDS-DMA: `size` bytes per lane from the per-lane global address `g` into
 // LDS at (wave-uniform) `lds_base` + lane * size.
 template <int SIZE>

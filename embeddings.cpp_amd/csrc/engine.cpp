@@ -628,8 +628,9 @@ extern "C" int32_t bertx_bench_gemm(int32_t fmt, int32_t N, int32_t K, int32_t M
         // -3: stamps; -3 - d: stamps + ablation d of gemmqw (kernels.h)
         const int diag = -3 - ablate;
         // stamped diagnostics: one launch, per-wave phase cycles to stderr
-        const int wm = tile_n == 128 ? 2 : 1;
-        const int nt = (Mp / GEMM_BM) * ((N + 256 / wm - 1) / (256 / wm));
+        // tile_n: 256 -> gemmqw 1 x 8, 128 -> gemmqw 2 x 4, 4 -> gemmqv BM 256, 5 -> gemmqv BM 128
+        const int wm = tile_n == 128 ? 2 : tile_n == 4 ? 4 : tile_n == 5 ? 5 : 1;
+        const int nt = wm >= 4 ? (Mp / 128) * ((N + 127) / 128) * 4 / 8 : (Mp / GEMM_BM) * ((N + 256 / wm - 1) / (256 / wm));
         uint64_t *dst = nullptr;
         HIP_RC(hipMalloc((void **)&dst, (size_t)nt * 32 * 8));
         for (int i = 0; i < 3; ++i) launch_gemm_q_stamped(W, (const uint16_t *)dx, Mp, (const float *)db, epi,

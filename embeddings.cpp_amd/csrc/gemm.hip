@@ -375,14 +375,16 @@ __global__ __launch_bounds__(512, 1) void gemmqw_kernel(DevWeight W, const h16 *
             uint32_t pk[4][2];                 // group g: 4 f16 of features 8g + 4hi + 0..3
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                h16 o[4];
+                float v[4];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const float v = bb[g][e] + acc[j][4 * g + e];
-                    o[e] = EPI == EPI_BIAS_GELU_F16 ? gelu_era(v) : (h16)v;
+                for (int e = 0; e < 4; ++e) v[e] = bb[g][e] + acc[j][4 * g + e];
+                if constexpr (EPI == EPI_BIAS_GELU_F16) {
+                    pk[g][0] = gelu2_era(v[0], v[1]);
+                    pk[g][1] = gelu2_era(v[2], v[3]);
+                } else {
+                    pk[g][0] = __builtin_bit_cast(uint32_t, h16x2{(h16)v[0], (h16)v[1]});
+                    pk[g][1] = __builtin_bit_cast(uint32_t, h16x2{(h16)v[2], (h16)v[3]});
                 }
-                pk[g][0] = __builtin_bit_cast(uint32_t, h16x2{o[0], o[1]});
-                pk[g][1] = __builtin_bit_cast(uint32_t, h16x2{o[2], o[3]});
             }
             // T21: half-exchange pairs (g, g+1) -> lanes 0-31 hold features 8g..8g+7,
             // lanes 32-63 hold 8g+8..8g+15 of the same token
@@ -434,11 +436,14 @@ void dispatch_qw(const DevWeight &W, const h16 *x, int M, const float *bias, int
 // X: 2-stage LDS-DMA ring (64 KiB at BM 256), one K-step ahead; W: 3-set
 // register ring, two K-steps ahead; one barrier per K-step.
 // ---------------------------------------------------------------------------
-template <int FMT, int EPI, int BM, int NS>
+template <int FMT, int EPI, int BM, int NS, bool STAMP = false>
 __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemmqv_kernel(DevWeight W, const h16 *__restrict__ X,
                                                         const float *__restrict__ bias, const void *__restrict__ res,
-                                                        void *__restrict__ out, int nN, int nTiles, ResLN rln)
+                                                        void *__restrict__ out, int nN, int nTiles, ResLN rln,
+                                                        uint64_t *__restrict__ stamps = nullptr)
 {
+    uint64_t ts[4];   // STAMP (diagnostics only): start / after prologue / after K loop / end
+    if constexpr (STAMP) ts[0] = __builtin_amdgcn_s_memtime();
     constexpr int BN = 128;
     constexpr int NJ = BM / 32;
     constexpr int XB = BM * GK * 2;            // bytes per X stage
@@ -506,6 +511,7 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     }
     lds_barrier();
 
+    if constexpr (STAMP) ts[1] = __builtin_amdgcn_s_memtime();
     const int sw = (lr >> 1) & 7;
     const int rbase = lr << 7;
     int st = 0;
@@ -581,6 +587,7 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 #undef EMB_VSTEP
 #undef EMB_ISSUE_XV
     wait_vmcnt<0>();
+    if constexpr (STAMP) ts[2] = __builtin_amdgcn_s_memtime();
 
     // ---- epilogue: lane holds token m0 + 32j + lr, features nw + 8g + 4hi + e ----
     if (nw >= N) return;                       // wave-uniform (N % 32 == 0)
@@ -630,14 +637,16 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             uint32_t pk[4][2];
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                h16 o[4];
+                float v[4];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const float v = bb[g][e] + acc[j][4 * g + e];
-                    o[e] = EPI == EPI_BIAS_GELU_F16 ? gelu_era(v) : (h16)v;
+                for (int e = 0; e < 4; ++e) v[e] = bb[g][e] + acc[j][4 * g + e];
+                if constexpr (EPI == EPI_BIAS_GELU_F16) {
+                    pk[g][0] = gelu2_era(v[0], v[1]);
+                    pk[g][1] = gelu2_era(v[2], v[3]);
+                } else {
+                    pk[g][0] = __builtin_bit_cast(uint32_t, h16x2{(h16)v[0], (h16)v[1]});
+                    pk[g][1] = __builtin_bit_cast(uint32_t, h16x2{(h16)v[2], (h16)v[3]});
                 }
-                pk[g][0] = __builtin_bit_cast(uint32_t, h16x2{o[0], o[1]});
-                pk[g][1] = __builtin_bit_cast(uint32_t, h16x2{o[2], o[3]});
             }
             h16 *orow = (h16 *)out + (size_t)(mrow + 32 * j) * N + nw + 8 * hi;
 #pragma unroll
@@ -653,6 +662,11 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
                 *(uint4 *)(orow + 8 * g) = v;
             }
         }
+    }
+    if constexpr (STAMP) {
+        ts[3] = __builtin_amdgcn_s_memtime();
+        if (lane == 0)
+            for (int i = 0; i < 4; ++i) stamps[((size_t)blockIdx.x * 4 + wave) * 4 + i] = ts[i];
     }
 }
 
@@ -695,8 +709,22 @@ int launch_gemm_q_stamped(const DevWeight &W, const uint16_t *X, int32_t M, cons
         case 192: dispatch_qw<FMT_Q4_0, 1, 0xd0>(W, x, M, bias, epi, res, out, s, ResLN(), stamps); break;
         default: dispatch_qw<FMT_Q4_0, 1, 0x10>(W, x, M, bias, epi, res, out, s, ResLN(), stamps); break;
         }
-    } else {
+    } else if (wm == 2) {
         dispatch_qw<FMT_Q4_0, 2, 0x10>(W, x, M, bias, epi, res, out, s, ResLN(), stamps);
+    } else {   // wm 4: gemmqv BM 256, wm 5: gemmqv BM 128 (4 waves per tile)
+        const int BM = wm == 4 ? 256 : 128;
+        const int nN = (W.N + 127) / 128, nt = (M / BM) * nN;
+        auto go = [&](auto kern) { kern<<<nt, 256, 0, s>>>(W, x, bias, res, out, nN, nt, ResLN(), stamps); };
+        if (wm == 4) {
+            if (epi == EPI_BIAS_F16) go(gemmqv_kernel<FMT_Q4_0, EPI_BIAS_F16, 256, 2, true>);
+            else if (epi == EPI_BIAS_GELU_F16) go(gemmqv_kernel<FMT_Q4_0, EPI_BIAS_GELU_F16, 256, 2, true>);
+            else go(gemmqv_kernel<FMT_Q4_0, EPI_BIAS_RES, 256, 2, true>);
+        } else {
+            if (epi == EPI_BIAS_F16) go(gemmqv_kernel<FMT_Q4_0, EPI_BIAS_F16, 128, 4, true>);
+            else if (epi == EPI_BIAS_GELU_F16) go(gemmqv_kernel<FMT_Q4_0, EPI_BIAS_GELU_F16, 128, 4, true>);
+            else go(gemmqv_kernel<FMT_Q4_0, EPI_BIAS_RES, 128, 4, true>);
+        }
+        return nt * 4 / 8;   // in units of 8 waves
     }
     return (M / GM) * ((W.N + BN - 1) / BN);
 }
