@@ -150,7 +150,7 @@ __global__ __launch_bounds__(256) void attention_kernel(const h16 *__restrict__ 
 // sentence's whole K and V (<= 512 x DH f16 each, 128 KiB at DH 64) are
 // brought into LDS ONCE by LDS-DMA; 16 waves x 32 queries then run with no
 // further global loads and no barriers.
-//   K image: [key][DH] rows, 16-B chunks XOR-swizzled by (key & 7) (via the
+//   K image: [key][DH] rows, 16-B chunks XOR-swizzled by kswz(key) (via the
 //            DMA source address), read as ds_read_b128 A fragments of S^T = K Q^T.
 //   V image: [key][DH] rows, chunks XOR-swizzled by ((key >> 1) & 1) << 2, read
 //            with ds_read_b64_tr_b16 as the transposed A fragments of
@@ -158,7 +158,17 @@ __global__ __launch_bounds__(256) void attention_kernel(const h16 *__restrict__ 
 // Q is pre-scaled by log2(e)/sqrt(dh) (f16), so S comes out in the exp2 domain;
 // keys past the sentence end are masked (only in the last 64-key block).
 // ---------------------------------------------------------------------------
-template <int DH>
+// K image chunk swizzle: the 16 lanes of a ds_read_b128 group read 16 rows
+// ({0-3,12-15,20-27} + 32n) at one chunk; XOR with (row >> 1) & 7 (128-B rows)
+// or (row >> 2) & 3 (64-B rows) puts them on 16 distinct 16-B bank slots.
+template <int CH, int VAR = 0>
+__device__ __forceinline__ int kswz(int row)
+{
+    if constexpr (VAR == 1) return row & (CH - 1);   // A/B only: the first (2-way conflicted) form
+    return CH == 8 ? ((row >> 1) & 7) : ((row >> 2) & 3);
+}
+
+template <int DH, int VAR = 0>
 __global__ __launch_bounds__(1024) void attention_lds_kernel(const h16 *__restrict__ qkv,
                                                              const int32_t *__restrict__ cu, int d, int nh,
                                                              float sl2, h16 *__restrict__ out)
@@ -182,7 +192,7 @@ __global__ __launch_bounds__(1024) void attention_lds_kernel(const h16 *__restri
         for (int i = w; i < ninstr; i += 16) {
             const int g = i * 64 + lane, row = g / CH, pc = g % CH;
             const int srow = min(row, len - 1);          // rows past the end: finite copies, masked / P = 0
-            const int ck = pc ^ (row & (CH - 1));
+            const int ck = pc ^ kswz<CH, VAR>(row);
             const int cv = pc ^ ((((row >> 1) & 1) << 2) & (CH - 1));
             glds<16>(kbase + (size_t)srow * ld + ck * 8, Kl + i * 1024);
             glds<16>(vbase + (size_t)srow * ld + cv * 8, Vl + i * 1024);
@@ -222,7 +232,7 @@ __global__ __launch_bounds__(1024) void attention_lds_kernel(const h16 *__restri
             const char *krow = Kl + row * RB;
 #pragma unroll
             for (int st = 0; st < DH / 16; ++st) {
-                const h16x8 a = *(const h16x8 *)(krow + (((2 * st + hi) ^ (row & (CH - 1))) << 4));
+                const h16x8 a = *(const h16x8 *)(krow + (((2 * st + hi) ^ kswz<CH, VAR>(row)) << 4));
                 s[kh] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, qf[st], s[kh], 0, 0, 0);
             }
         }
@@ -299,16 +309,23 @@ __global__ __launch_bounds__(1024) void attention_lds_kernel(const h16 *__restri
     }
 }
 
+int g_att_variant = 0;   // benches only (bertx_bench_attention)
+
 void launch_attention(const uint16_t *qkv, const int32_t *cu, int32_t n_seqs, int32_t max_len, int32_t n_head,
                       int32_t d, uint16_t *out, hipStream_t s)
 {
     const int dh = d / n_head;
     const float sl2 = (1.0f / sqrtf((float)dh)) * 1.4426950408889634f;
     if (max_len <= ATT_LDS_MAX && (dh == 64 || dh == 32)) {
-        if (dh == 64)
-            attention_lds_kernel<64><<<n_seqs * n_head, 1024, 0, s>>>((const h16 *)qkv, cu, d, n_head, sl2, (h16 *)out);
-        else
-            attention_lds_kernel<32><<<n_seqs * n_head, 1024, 0, s>>>((const h16 *)qkv, cu, d, n_head, sl2, (h16 *)out);
+        const dim3 g(n_seqs * n_head), blk(1024);
+        if (dh == 64) {
+            if (g_att_variant == 1)
+                attention_lds_kernel<64, 1><<<g, blk, 0, s>>>((const h16 *)qkv, cu, d, n_head, sl2, (h16 *)out);
+            else
+                attention_lds_kernel<64, 0><<<g, blk, 0, s>>>((const h16 *)qkv, cu, d, n_head, sl2, (h16 *)out);
+        } else {
+            attention_lds_kernel<32, 0><<<g, blk, 0, s>>>((const h16 *)qkv, cu, d, n_head, sl2, (h16 *)out);
+        }
         return;
     }
     const int nqt = (max_len + ATT_QT - 1) / ATT_QT;

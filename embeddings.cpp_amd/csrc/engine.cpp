@@ -673,3 +673,46 @@ extern "C" int32_t bertx_bench_gemm(int32_t fmt, int32_t N, int32_t K, int32_t M
     for (char *p : {dq, dd, dx, db, dr, dout}) (void)hipFree(p);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+// ---------------------------------------------------------------------------
+// attention micro-benchmark (bert_hip.h): n_seqs sentences of `len` tokens,
+// random Q/K/V, device-timed launches of variant `variant`
+// ---------------------------------------------------------------------------
+extern "C" int32_t bertx_bench_attention(int32_t n_seqs, int32_t len, int32_t n_head, int32_t dh, int32_t variant,
+                                         int32_t iters, float *avg_us)
+{
+    using namespace emb;
+    if (n_seqs <= 0 || len <= 0 || iters <= 0 || hip_device_count() == 0) return -1;
+    const int d = n_head * dh;
+    const size_t T = (size_t)n_seqs * len, rows = T + 256;
+    std::vector<uint16_t> hq(rows * 3 * d);
+    uint32_t st = 777u;
+    for (auto &v : hq) { st = st * 1664525u + 1013904223u; v = f32_to_f16(((st >> 8) / 16777216.0f - 0.5f) * 2.0f); }
+    std::vector<int32_t> hcu((size_t)n_seqs + 1);
+    for (int i = 0; i <= n_seqs; ++i) hcu[(size_t)i] = i * len;
+    uint16_t *dq = nullptr, *dout = nullptr;
+    int32_t *dcu = nullptr;
+    HIP_RC(hipSetDevice(0));
+    HIP_RC(hipMalloc((void **)&dq, hq.size() * 2));
+    HIP_RC(hipMemcpy(dq, hq.data(), hq.size() * 2, hipMemcpyHostToDevice));
+    HIP_RC(hipMalloc((void **)&dcu, hcu.size() * 4));
+    HIP_RC(hipMemcpy(dcu, hcu.data(), hcu.size() * 4, hipMemcpyHostToDevice));
+    HIP_RC(hipMalloc((void **)&dout, rows * d * 2));
+    g_att_variant = variant;
+    for (int i = 0; i < 3; ++i) launch_attention(dq, dcu, n_seqs, len, n_head, d, dout, nullptr);
+    hipEvent_t a, b;
+    HIP_RC(hipEventCreate(&a));
+    HIP_RC(hipEventCreate(&b));
+    HIP_RC(hipEventRecord(a, nullptr));
+    for (int i = 0; i < iters; ++i) launch_attention(dq, dcu, n_seqs, len, n_head, d, dout, nullptr);
+    HIP_RC(hipEventRecord(b, nullptr));
+    HIP_RC(hipEventSynchronize(b));
+    g_att_variant = 0;
+    float ms = 0.f;
+    HIP_RC(hipEventElapsedTime(&ms, a, b));
+    *avg_us = ms * 1000.f / (float)iters;
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    for (void *p : {(void *)dq, (void *)dcu, (void *)dout}) (void)hipFree(p);
+    return 0;
+}

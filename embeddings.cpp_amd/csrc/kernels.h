@@ -93,6 +93,9 @@ void launch_embed_ln(const DevTable &word, const DevTable &type, const DevTable 
 void launch_layernorm(const uint16_t *yh, int32_t T, int32_t d, const float *w, const float *b, uint16_t *xh,
                       float2 *stats, hipStream_t s);
 
+// Benches only: attention kernel variant (bertx_bench_attention).
+extern int g_att_variant;
+
 // Per (sentence, head) softmax(Q K^T / sqrt(dh)) V over the sentence's own keys.
 void launch_attention(const uint16_t *qkv, const int32_t *cu, int32_t n_seqs, int32_t max_len, int32_t n_head,
                       int32_t d, uint16_t *out, hipStream_t s);

@@ -82,6 +82,14 @@ BERT_API int32_t bertx_test_gemm(int32_t fmt, int32_t N, int32_t K, const void *
 BERT_API int32_t bertx_bench_gemm(int32_t fmt, int32_t N, int32_t K, int32_t M, int32_t epi, int32_t tile_n,
                                   int32_t ablate, int32_t iters, float *avg_us);
 
+/*
+ * Attention micro-benchmark on random operands (device 0): average device time
+ * of `iters` launches for n_seqs sentences of `len` tokens, n_head heads of size
+ * dh; variant 0 = production kernel (others: A/B builds, see attention.hip).
+ */
+BERT_API int32_t bertx_bench_attention(int32_t n_seqs, int32_t len, int32_t n_head, int32_t dh, int32_t variant,
+                                       int32_t iters, float *avg_us);
+
 BERT_API const char *bertx_version(void);
 
 #ifdef __cplusplus
