@@ -70,6 +70,8 @@ def load_lib(path=None):
                                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), c_i32p]
     L.bertx_quantize_file.restype = c_i32
     L.bertx_quantize_file.argtypes = [ctypes.c_char_p, ctypes.c_char_p, c_i32]
+    L.bertx_convert_hf.restype = c_i32
+    L.bertx_convert_hf.argtypes = [ctypes.c_char_p, ctypes.c_char_p, c_i32]
     L.bertx_test_gemm.restype = c_i32
     L.bertx_test_gemm.argtypes = [c_i32, c_i32, c_i32, vp, c_f32p, c_i32, vp, c_i32, vp, vp, c_i32]
     L.bertx_bench_gemm.restype = c_i32

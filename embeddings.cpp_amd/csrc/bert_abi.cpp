@@ -386,6 +386,11 @@ int32_t bertx_quantize_file(const char *fin, const char *fout, int32_t itype)
     return emb::quantize_file(fin, fout, itype, false);
 }
 
+int32_t bertx_convert_hf(const char *dir_model, const char *fname_out, int32_t ftype)
+{
+    return emb::convert_hf_dir(dir_model, fname_out, ftype);
+}
+
 const char *bertx_version(void) { return "embeddings.cpp_amd 0.1 (gfx950)"; }
 
 }  // extern "C"

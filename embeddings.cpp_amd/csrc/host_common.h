@@ -71,5 +71,7 @@ void dequant_row(int fmt, const uint8_t *src, float *dst, int64_t k);
 
 // Native quantizer (mirrors models/quantize.cpp:27-268; itype 2, 3, or 8).
 int quantize_file(const char *in, const char *out, int itype, bool verbose);
+// HF directory (config.json, vocab.txt, model.safetensors) -> model file (converter.cpp)
+int convert_hf_dir(const std::string &dir, const std::string &fname_out, int ftype);
 
 }  // namespace emb

@@ -58,6 +58,13 @@ BERT_API int32_t bertx_kernel_stats(struct bert_ctx *ctx, int32_t idx, const cha
  * 2 (q4_0), 3 (q4_1) or 8 (q8_0, extension).  Returns 0 on success. */
 BERT_API int32_t bertx_quantize_file(const char *fname_in, const char *fname_out, int32_t itype);
 
+/* Native converter (mirrors models/convert-to-ggml.py:1-113): a local HF
+ * BERT directory (config.json, vocab.txt, model.safetensors or a sharded
+ * model.safetensors.index.json) -> model file, ftype 0 (f32) or 1 (f16:
+ * 2-D weights only).  Same bytes as the reference script writes.  Returns 0
+ * on success. */
+BERT_API int32_t bertx_convert_hf(const char *dir_model, const char *fname_out, int32_t ftype);
+
 /*
  * Per-kernel parity hooks (host buffers in/out, runs synchronously on the
  * first device).  w_rows: the weight exactly as the model file stores it

@@ -179,3 +179,97 @@ def test_synthetic_model_writer_roundtrip(lib, oracle, tmp_path, monkeypatch):
     assert m.hparams()[:6] == [o.n_vocab, o.n_max_tokens, o.n_embd, o.n_intermediate, o.n_head, o.n_layer]
     assert m.hparams()[:6] == [300, 64, 64, 128, 2, 1]
     assert ctypes.sizeof(ctypes.c_int32) == 4
+
+
+# ---- native converter vs the reference converter's committed output ----
+
+def _parse_model_file(path):
+    """-> (hparams[7], vocab list of bytes, [(name, np.ndarray f32 in torch shape)])."""
+    import struct
+    b = open(path, "rb").read()
+    hp = struct.unpack("8i", b[:32])[1:]
+    o, vocab = 32, []
+    for _ in range(hp[0]):
+        n = struct.unpack("i", b[o:o + 4])[0]
+        vocab.append(b[o + 4:o + 4 + n])
+        o += 4 + n
+    tens = []
+    while o < len(b):
+        nd, nl, ft = struct.unpack("3i", b[o:o + 12])
+        o += 12
+        ne = struct.unpack("%di" % nd, b[o:o + 4 * nd])
+        o += 4 * nd
+        name = b[o:o + nl].decode()
+        o += nl
+        cnt = int(np.prod(ne)) if nd else 1
+        dt = np.float32 if ft == 0 else np.float16
+        a = np.frombuffer(b, dt, cnt, o).astype(np.float32).reshape(tuple(reversed(ne)))
+        o += cnt * np.dtype(dt).itemsize
+        tens.append((name, a))
+    return hp, vocab, tens
+
+
+def _write_hf_dir(d, hp, vocab, tens, prefix="", extra=True, shards=1):
+    import json as _json
+    from safetensors.numpy import save_file
+    os.makedirs(d, exist_ok=True)
+    cfg = dict(vocab_size=hp[0], max_position_embeddings=hp[1], hidden_size=hp[2], intermediate_size=hp[3],
+               num_attention_heads=hp[4], num_hidden_layers=hp[5], model_type="bert", layer_norm_eps=1e-12)
+    with open(os.path.join(d, "config.json"), "w") as f:
+        _json.dump(cfg, f)
+    with open(os.path.join(d, "vocab.txt"), "wb") as f:
+        f.write(b"".join(v + b"\n" for v in vocab))
+    t = {prefix + n: np.ascontiguousarray(a) for n, a in tens}
+    if extra:   # what BertModel checkpoints also hold; the reference skips them (convert-to-ggml.py:86-87)
+        t[prefix + "pooler.dense.weight"] = np.zeros((hp[2], hp[2]), np.float32)
+        t[prefix + "pooler.dense.bias"] = np.zeros((hp[2],), np.float32)
+        t[prefix + "embeddings.position_ids"] = np.arange(hp[1], dtype=np.float32)[None]
+    names = sorted(t)
+    if shards == 1:
+        save_file(t, os.path.join(d, "model.safetensors"))
+    else:
+        wm = {}
+        for s in range(shards):
+            part = {n: t[n] for n in names[s::shards]}
+            fn = "model-%05d-of-%05d.safetensors" % (s + 1, shards)
+            save_file(part, os.path.join(d, fn))
+            wm.update({n: fn for n in part})
+        with open(os.path.join(d, "model.safetensors.index.json"), "w") as f:
+            _json.dump({"metadata": {}, "weight_map": wm}, f)
+
+
+@pytest.mark.parametrize("tiny", ["tiny32", "tiny64"])
+@pytest.mark.parametrize("layout", [dict(), dict(prefix="bert.", shards=3)])
+def test_converter_bytes_match_reference_script(lib, tmp_path, tiny, layout):
+    """build/bin/convert (converter.cpp) on an HF directory holding the weights
+    of the committed fixtures == the bytes models/convert-to-ggml.py wrote for
+    them (tests/golden/<tiny>/ggml-model-{f32,f16}.bin, make_golden.py)."""
+    ref32 = os.path.join(GOLDEN, tiny, "ggml-model-f32.bin")
+    hp, vocab, tens = _parse_model_file(ref32)
+    d = str(tmp_path / "hf")
+    _write_hf_dir(d, hp, vocab, tens, **layout)
+    for ft, fn in ((0, "ggml-model-f32.bin"), (1, "ggml-model-f16.bin")):
+        out = str(tmp_path / fn)
+        assert lib.bertx_convert_hf(d.encode(), out.encode(), ft) == 0
+        assert open(out, "rb").read() == open(os.path.join(GOLDEN, tiny, fn), "rb").read(), fn
+
+
+def test_converter_cli_and_errors(lib, tmp_path):
+    hp, vocab, tens = _parse_model_file(os.path.join(GOLDEN, "tiny32", "ggml-model-f32.bin"))
+    d = str(tmp_path / "hf")
+    _write_hf_dir(d, hp, vocab, tens)
+    exe = os.path.join(ROOT, "build", "bin", "convert")
+    r = subprocess.run([exe, d, "1"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert open(os.path.join(d, "ggml-model-f16.bin"), "rb").read() == \
+        open(os.path.join(GOLDEN, "tiny32", "ggml-model-f16.bin"), "rb").read()
+    assert subprocess.run([exe, d, "2"], capture_output=True).returncode != 0      # Invalid ftype
+    assert subprocess.run([exe], capture_output=True).returncode != 0               # usage
+    # missing tensor / short vocab / no checkpoint: refused, nothing claimed
+    bad = str(tmp_path / "bad")
+    _write_hf_dir(bad, hp, vocab, [t for t in tens if "layer.1.output.dense.bias" not in t[0]])
+    assert lib.bertx_convert_hf(bad.encode(), str(tmp_path / "x.bin").encode(), 0) != 0
+    _write_hf_dir(bad, hp, vocab[:-5], tens)
+    assert lib.bertx_convert_hf(bad.encode(), str(tmp_path / "x.bin").encode(), 0) != 0
+    os.remove(os.path.join(bad, "model.safetensors"))
+    assert lib.bertx_convert_hf(bad.encode(), str(tmp_path / "x.bin").encode(), 0) != 0
