@@ -23,6 +23,15 @@ __device__ __forceinline__ float wave_sum(float v)
 
 __device__ __forceinline__ h16x2 as_h2(uint32_t u) { return __builtin_bit_cast(h16x2, u); }
 __device__ __forceinline__ h16 as_h(uint16_t u) { return __builtin_bit_cast(h16, u); }
+// (x & vmask) | smagic as ONE v_and_or_b32: gfx9 VOP3 encodes no literal and reads at
+// most one SGPR, so the compiler splits the two-constant form into v_and + v_or;
+// here the mask lives in a VGPR (hoisted) and the magic in an SGPR.
+__device__ __forceinline__ uint32_t and_or_vs(uint32_t x, uint32_t vmask, uint32_t smagic)
+{
+    uint32_t r;
+    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(vmask), "s"(smagic));
+    return r;
+}
 
 // ggml-era GELU (tanh form) on an f16-rounded input, result rounded to f16 --
 // the value ggml's GGML_GELU_FP16 table holds (bert.cpp:1063).  Evaluated as

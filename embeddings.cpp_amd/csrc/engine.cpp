@@ -3,12 +3,16 @@
 #include "engine.h"
 
 #include <algorithm>
+#include <functional>
+#include <map>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
 namespace emb {
+
+int g_weight_layout = 1;   // kernels.h
 
 #define HIP_OK(expr)                                                                                     \
     do {                                                                                                 \
@@ -58,14 +62,71 @@ struct Piece {
 };
 
 // Linear weight [N][K] (file rows) -> K-step-major device layout (kernels.h).
+// Layout 1 (kernels.h, gemm16.hip): lane-order records per (K-step, 32-feature group).
+void repack_linear_l16(const std::vector<const HostTensor *> &parts, int fmt_dev, int N, int K, Piece &qs,
+                       Piece &dpl, Piece &mpl)
+{
+    const size_t G = (size_t)N / 32;
+    const size_t QB = fmt_dev == FMT_F16 ? 64 : fmt_dev == FMT_Q8_0 ? 32 : 16;
+    qs.bytes.assign((size_t)(K / 64) * G * 64 * QB, 0);
+    if (fmt_dev != FMT_F16) dpl.bytes.assign((size_t)N * (K / 32) * 2, 0);
+    if (fmt_dev == FMT_Q4_1) mpl.bytes.assign((size_t)N * (K / 32) * 2, 0);
+    uint16_t *dd = (uint16_t *)dpl.bytes.data();
+    uint16_t *mm = fmt_dev == FMT_Q4_1 ? (uint16_t *)mpl.bytes.data() : nullptr;
+    static const int pos4[4] = {0, 2, 1, 3};
+    std::vector<float> row((size_t)K);
+    int n = 0;
+    for (const HostTensor *t : parts) {
+        const size_t rb = fmt_row_bytes(t->fmt, K), bb = fmt_block_bytes(t->fmt);
+        for (int r = 0; r < t->ne1; ++r, ++n) {
+            const uint8_t *src = t->bytes.data() + rb * r;
+            const size_t grp = (size_t)n / 32;
+            const int a = (n % 32) / 16, f = n % 16;
+            for (int blk = 0; blk < K / 32; ++blk) {
+                const size_t ks = (size_t)blk / 2;
+                const int u = 2 * a + (blk & 1);
+                const size_t rec0 = (ks * G + grp) * 64;            // lane-record index of lane 0
+                const size_t di = ((ks * G + grp) * 16 + f) * 4 + u;
+                for (int e = 0; e < 32; ++e) {
+                    const int g = e / 8, i = e % 8;
+                    uint8_t *o = qs.bytes.data() + (rec0 + 16 * g + f) * QB;
+                    const int k = 32 * blk + e;
+                    if (fmt_dev == FMT_F16) {
+                        uint16_t h;
+                        if (t->fmt == FMT_F16) std::memcpy(&h, src + 2 * k, 2);
+                        else { float v; std::memcpy(&v, src + 4 * k, 4); h = f32_to_f16(v); }
+                        std::memcpy(o + 16 * u + 2 * i, &h, 2);
+                    } else if (fmt_dev == FMT_Q8_0) {
+                        const int8_t q = (int8_t)src[bb * blk + 2 + e];
+                        o[8 * u + 4 * (i / 4) + pos4[i % 4]] = (uint8_t)((uint8_t)q ^ 0x80u);
+                    } else {
+                        const uint8_t *nib = src + bb * blk + (fmt_dev == FMT_Q4_1 ? 4 : 2);
+                        const uint32_t q = e < 16 ? (nib[e] & 15u) : (uint32_t)(nib[e - 16] >> 4);
+                        uint32_t w;
+                        std::memcpy(&w, o + 4 * u, 4);
+                        w |= q << (4 * (i / 2) + 16 * (i % 2));
+                        std::memcpy(o + 4 * u, &w, 4);
+                    }
+                }
+                if (fmt_dev != FMT_F16) std::memcpy(&dd[di], src + bb * blk, 2);
+                if (mm) std::memcpy(&mm[di], src + bb * blk + 2, 2);
+            }
+        }
+    }
+}
+
 void repack_linear(const std::vector<const HostTensor *> &parts, int fmt_dev, Piece &qs, Piece &dpl, Piece &mpl,
-                   int &N_out, int &K_out)
+                   int &N_out, int &K_out, int layout)
 {
     const int K = parts[0]->ne0;
     int N = 0;
     for (const HostTensor *t : parts) N += t->ne1;
     N_out = N;
     K_out = K;
+    if (layout == 1) {
+        repack_linear_l16(parts, fmt_dev, N, K, qs, dpl, mpl);
+        return;
+    }
     const int KS = K / 64;
     if (fmt_dev == FMT_F16) {
         qs.bytes.assign((size_t)N * K * 2, 0);
@@ -190,6 +251,10 @@ void Device::upload(const HostModel &m)
         return;
     }
     wfmt_ = (hp_.ftype == FMT_F32 || hp_.ftype == FMT_F16) ? FMT_F16 : hp_.ftype;
+    {
+        const char *e = std::getenv("BERT_GEMM_LAYOUT");
+        layout_ = (e && (*e == '0' || *e == '1')) ? *e - '0' : g_weight_layout;
+    }
     std::vector<Piece> pieces;
     pieces.reserve(16 + 24 * (size_t)hp_.n_layer);
     auto add = [&](Piece &&p) -> size_t { pieces.push_back(std::move(p)); return pieces.size() - 1; };
@@ -211,7 +276,7 @@ void Device::upload(const HostModel &m)
     auto linear = [&](std::vector<const HostTensor *> parts) -> LinIdx {
         Piece q, dd, mm;
         LinIdx r;
-        repack_linear(parts, wfmt_, q, dd, mm, r.N, r.K);
+        repack_linear(parts, wfmt_, q, dd, mm, r.N, r.K, layout_);
         r.q = add(std::move(q)); r.d = add(std::move(dd)); r.m = add(std::move(mm));
         return r;
     };
@@ -257,7 +322,7 @@ void Device::upload(const HostModel &m)
     ln_e_b_ = (float *)P(lnb);
     auto mk_lin = [&](const LinIdx &x) {
         DevWeight w;
-        w.fmt = wfmt_; w.N = x.N; w.K = x.K;
+        w.fmt = wfmt_; w.N = x.N; w.K = x.K; w.layout = layout_;
         w.qs = P(x.q); w.d = (const uint16_t *)P(x.d); w.m = (const uint16_t *)P(x.m);
         return w;
     };
@@ -541,7 +606,9 @@ extern "C" int32_t bertx_test_gemm(int32_t fmt, int32_t N, int32_t K, const void
     const int fdev = (fmt == FMT_F32 || fmt == FMT_F16) ? FMT_F16 : fmt;
     Piece q, dd, mm;
     int n_out = 0, k_out = 0;
-    repack_linear({&t}, fdev, q, dd, mm, n_out, k_out);
+    // tile_n: 0 production; 128 / 256 gemm.hip tiles (layout 0); 0x1000 | cfg gemm16 (layout 1)
+    const int layout = tile_n == 0 ? g_weight_layout : (tile_n & 0x1000) ? 1 : 0;
+    repack_linear({&t}, fdev, q, dd, mm, n_out, k_out, layout);
     const int Mp = (int)align_up((size_t)M, GEMM_BM);
     const size_t osz = 2;   // f16 out for every epilogue
     char *dq = nullptr, *dd_ = nullptr, *dm = nullptr, *dx = nullptr, *db = nullptr, *dr = nullptr, *dout = nullptr;
@@ -569,10 +636,12 @@ extern "C" int32_t bertx_test_gemm(int32_t fmt, int32_t N, int32_t K, const void
     }
     DevWeight W;
     W.fmt = fdev; W.N = n_out; W.K = k_out;
-    W.qs = dq; W.d = (const uint16_t *)dd_; W.m = (const uint16_t *)dm;
-    g_force_bn = tile_n;
+    W.qs = dq; W.d = (const uint16_t *)dd_; W.m = (const uint16_t *)dm; W.layout = layout;
+    g_force_bn = layout == 0 ? tile_n : 0;
+    g_gemm16_cfg = layout == 1 ? (tile_n & 0xff) : 0;
     launch_gemm(W, (const uint16_t *)dx, Mp, (const float *)db, epi, (const void *)dr, dout, nullptr);
     g_force_bn = 0;
+    g_gemm16_cfg = 0;
     HIP_RC(hipGetLastError());
     HIP_RC(hipDeviceSynchronize());
     HIP_RC(hipMemcpy(out, dout, (size_t)M * N * osz, hipMemcpyDeviceToHost));
@@ -617,11 +686,15 @@ extern "C" int32_t bertx_bench_gemm(int32_t fmt, int32_t N, int32_t K, int32_t M
     DevWeight W;
     W.fmt = fdev; W.N = N; W.K = K;
     W.qs = dq; W.d = (const uint16_t *)dd; W.m = (const uint16_t *)dd;
-    auto launch = [&]() {
-        g_force_bn = tile_n;
+    // tile_n 0x1000 | cfg: gemm16 (layout 1) with that config; otherwise gemm.hip (layout 0)
+    W.layout = (tile_n & 0x1000) ? 1 : 0;
+    std::function<void()> launch = [&]() {
+        g_force_bn = W.layout ? 0 : tile_n;
+        g_gemm16_cfg = W.layout ? (tile_n & 0xff) : 0;
         g_gemm_variant = ablate == -2 ? 2 : 0;   // -2: gemmqw everywhere
         launch_gemm(W, (const uint16_t *)dx, Mp, (const float *)db, epi, (const void *)dr, dout, nullptr);
         g_force_bn = 0;
+        g_gemm16_cfg = 0;
         g_gemm_variant = 0;
     };
     if (ablate <= -3 && ablate >= -300 && fdev == FMT_Q4_0) {
@@ -631,31 +704,71 @@ extern "C" int32_t bertx_bench_gemm(int32_t fmt, int32_t N, int32_t K, int32_t M
         // tile_n: 256 -> gemmqw 1 x 8, 128 -> gemmqw 2 x 4, 4 -> gemmqv BM 256, 5 -> gemmqv BM 128
         const int wm = tile_n == 128 ? 2 : tile_n == 4 ? 4 : tile_n == 5 ? 5 : 1;
         const int nt = wm >= 4 ? (Mp / 128) * ((N + 127) / 128) * 4 / 8 : (Mp / GEMM_BM) * ((N + 256 / wm - 1) / (256 / wm));
+        // per wave: 4 s_memtime phase stamps (gemmqw: + realtime start/end and the CU id)
+        const int SW = wm == 1 ? 8 : 4;
         uint64_t *dst = nullptr;
-        HIP_RC(hipMalloc((void **)&dst, (size_t)nt * 32 * 8));
-        for (int i = 0; i < 3; ++i) launch_gemm_q_stamped(W, (const uint16_t *)dx, Mp, (const float *)db, epi,
-                                                          (const void *)dr, dout, nullptr, wm, dst, diag);
+        HIP_RC(hipMalloc((void **)&dst, (size_t)nt * 8 * SW * 8));
+        HIP_RC(hipMemset(dst, 0, (size_t)nt * 8 * SW * 8));
+        // 3 + iters stamped launches; the events time the last iters, the stamps are the last one's
+        hipEvent_t e0, e1;
+        HIP_RC(hipEventCreate(&e0));
+        HIP_RC(hipEventCreate(&e1));
+        for (int i = 0; i < 3 + iters; ++i) {
+            if (i == 3) HIP_RC(hipEventRecord(e0, nullptr));
+            launch_gemm_q_stamped(W, (const uint16_t *)dx, Mp, (const float *)db, epi, (const void *)dr, dout,
+                                  nullptr, wm, dst, diag);
+        }
+        HIP_RC(hipEventRecord(e1, nullptr));
         HIP_RC(hipDeviceSynchronize());
-        std::vector<uint64_t> h((size_t)nt * 32);
+        float st_ms = 0.f;
+        HIP_RC(hipEventElapsedTime(&st_ms, e0, e1));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        std::vector<uint64_t> h((size_t)nt * 8 * SW);
         HIP_RC(hipMemcpy(h.data(), dst, h.size() * 8, hipMemcpyDeviceToHost));
         (void)hipFree(dst);
         std::vector<double> pro, loop, epi_c, wg;
-        uint64_t t0 = ~0ull, t1 = 0;
-        for (int b = 0; b < nt; ++b)
+        uint64_t r0 = ~0ull, r1 = 0;
+        double busy = 0;                         // sum over tiles of (last wave end - first wave start), realtime
+        std::map<uint64_t, double> cu_busy;      // per CU
+        for (int b = 0; b < nt; ++b) {
+            uint64_t b0 = ~0ull, b1 = 0, cu = 0;
             for (int w = 0; w < 8; ++w) {
-                const uint64_t *p = &h[((size_t)b * 8 + w) * 4];
+                const uint64_t *p = &h[((size_t)b * 8 + w) * SW];
                 if (!p[3]) continue;
                 pro.push_back((double)(p[1] - p[0]));
                 loop.push_back((double)(p[2] - p[1]) / (K / 64));
                 epi_c.push_back((double)(p[3] - p[2]));
                 wg.push_back((double)(p[3] - p[0]));
-                t0 = std::min(t0, p[0]);
-                t1 = std::max(t1, p[3]);
+                if (SW == 8 && p[5]) {
+                    b0 = std::min(b0, p[4]); b1 = std::max(b1, p[5]);
+                    cu = (p[6] >> 32) * 4096 + ((p[6] >> 8) & 0xfff);   // xcc, (se, sh, cu)
+                }
             }
+            if (b1 > b0) {
+                r0 = std::min(r0, b0); r1 = std::max(r1, b1);
+                busy += (double)(b1 - b0);
+                cu_busy[cu] += (double)(b1 - b0);
+            }
+        }
         auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v.empty() ? 0.0 : v[v.size() / 2]; };
         std::fprintf(stderr, "stamps diag=%d N=%d K=%d M=%d wm=%d: tiles %d  median cycles: prologue %.0f  per-K-step %.0f  "
-                     "epilogue %.0f  wave total %.0f  | kernel span %.0f\n", diag, N, K, Mp, wm, nt, med(pro), med(loop),
-                     med(epi_c), med(wg), (double)(t1 - t0));
+                     "epilogue %.0f  wave total %.0f", diag, N, K, Mp, wm, nt, med(pro), med(loop), med(epi_c), med(wg));
+        if (r1 > r0) {
+            // s_memrealtime: 100 MHz
+            const double span_us = (double)(r1 - r0) / 100.0;
+            std::fprintf(stderr, "  | realtime span %.1f us, tile avg %.2f us, CUs used %zu, CU busy %.1f%%",
+                         span_us, busy / nt / 100.0, cu_busy.size(), 100.0 * busy / (double)(r1 - r0) / cu_busy.size());
+        }
+        std::fprintf(stderr, "  | stamped launches avg %.1f us\n", st_ms * 1000.0 / iters);
+    }
+    if (ablate <= -3 && ablate >= -300 && fdev == FMT_Q4_0 && (tile_n == 0 || tile_n == 256)) {
+        // time the diagnostic variant itself (same build without the stamps)
+        const int diag = -3 - ablate;
+        launch = [&, diag]() {
+            launch_gemm_q_stamped(W, (const uint16_t *)dx, Mp, (const float *)db, epi, (const void *)dr, dout,
+                                  nullptr, 1, nullptr, diag);
+        };
     }
     for (int i = 0; i < 3; ++i) launch();
     hipEvent_t a, b;

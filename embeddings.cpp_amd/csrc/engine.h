@@ -98,6 +98,7 @@ private:
     float *ln_e_w_ = nullptr, *ln_e_b_ = nullptr;
     std::vector<DevLayer> layers_;
     int wfmt_ = FMT_F16;
+    int layout_ = 1;                // DevWeight::layout of the linear weights
 
     // workspace
     int64_t cap_tokens_ = 0, cap_seqs_ = 0;

@@ -32,6 +32,8 @@
 #include "host_common.h"
 #include "kernels.h"
 
+#include <type_traits>
+
 namespace emb {
 
 namespace {
@@ -91,7 +93,7 @@ struct QRegsQ4 {
         h16x8 a;
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
-            h16x2 hh = as_h2(((w >> (4 * p)) & 0x000F000Fu) | 0x64006400u) + off;
+            h16x2 hh = as_h2(and_or_vs(w >> (4 * p), 0x000F000Fu, 0x64006400u)) + off;
             hh = FMT == FMT_Q4_1 ? hh * d2 + m2 : hh * d2;
             a[2 * p] = hh[0];
             a[2 * p + 1] = hh[1];
@@ -177,8 +179,8 @@ __global__ __launch_bounds__(512, 1) void gemmqw_kernel(DevWeight W, const h16 *
     // STAMP (diagnostics build only): s_memtime at start / after the prologue /
     // after the K loop / after the epilogue, per wave, into stamps[]
     constexpr bool STAMP = (DIAG & 0x10) != 0;
-    uint64_t ts[4];
-    if constexpr (STAMP) ts[0] = __builtin_amdgcn_s_memtime();
+    uint64_t ts[4], rt0 = 0;
+    if constexpr (STAMP) { ts[0] = __builtin_amdgcn_s_memtime(); rt0 = __builtin_amdgcn_s_memrealtime(); }
     constexpr int WN = 8 / WM;                 // waves along the features
     constexpr int BN = 32 * WN;                // 256 (WM 1) or 128 (WM 2)
     constexpr int TM = GM / WM;                // tokens per wave
@@ -187,7 +189,7 @@ __global__ __launch_bounds__(512, 1) void gemmqw_kernel(DevWeight W, const h16 *
     constexpr int P = QRegs<FMT>::LOADS + 4;   // vector-memory ops issued per K-step per wave
     __shared__ __attribute__((aligned(16))) char smem[XS * X_BYTES];
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int b = blockIdx.x, xcd = b & 7, qq = nTiles >> 3, rr = nTiles & 7;
     const int t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
     const int m0 = (t / nN) * GM, n0 = (t % nN) * BN;
@@ -259,7 +261,28 @@ __global__ __launch_bounds__(512, 1) void gemmqw_kernel(DevWeight W, const h16 *
             CUR.pin_all();                                                                                \
         }                                                                                                 \
         const char *xs = smem + st * X_BYTES + rbase;                                                     \
-        if constexpr (DIAG & 0x20) {                                                                      \
+        if constexpr ((DIAG & 0x100) && NJ == 8) {                                                        \
+            /* B reads two ahead in a 3-register rotation, A of k-slice kk+1 expanded */                  \
+            /* during kk; sched_group_barrier pins [DS read, 2 VALU, MFMA] per slot */                    \
+            h16x8 bq[3];                                                                                  \
+            bq[0] = *(const h16x8 *)(xs + (0 << 12) + ((hi ^ sw) << 4));                                  \
+            bq[1] = *(const h16x8 *)(xs + (1 << 12) + ((hi ^ sw) << 4));                                  \
+            h16x8 a = CUR.frag(0), an = a;                                                                \
+            _Pragma("unroll") for (int idx = 0; idx < 32; ++idx)                                          \
+            {                                                                                             \
+                const int kk = idx >> 3, j = idx & 7;                                                     \
+                if (idx + 2 < 32) {                                                                       \
+                    const int i2 = idx + 2;                                                               \
+                    bq[i2 % 3] = *(const h16x8 *)(xs + ((i2 & 7) << 12) + (((2 * (i2 >> 3) + hi) ^ sw) << 4)); \
+                }                                                                                         \
+                if (j == 0 && kk > 0) a = an;                                                             \
+                if (j == 1 && kk < 3) an = CUR.frag(kk + 1);                                              \
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bq[idx % 3], acc[j], 0, 0, 0);         \
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                        \
+                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);                                        \
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                        \
+            }                                                                                             \
+        } else if constexpr (DIAG & 0x20) {                                                               \
             /* software-pipelined: B fragments and A dequant of k-slice kk+1 issued */                   \
             /* between the MFMAs of kk (sched_group_barrier pins the interleave) */                       \
             h16x8 bc[NJ], bnx[NJ];                                                                        \
@@ -405,8 +428,15 @@ __global__ __launch_bounds__(512, 1) void gemmqw_kernel(DevWeight W, const h16 *
     }
     if constexpr (STAMP) {
         ts[3] = __builtin_amdgcn_s_memtime();
-        if (lane == 0)
-            for (int i = 0; i < 4; ++i) stamps[((size_t)blockIdx.x * 8 + wave) * 4 + i] = ts[i];
+        const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
+        // HW_ID (CU / SE / SIMD) and XCC_ID: which CU ran this tile
+        const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);
+        if (lane == 0) {
+            uint64_t *o = stamps + ((size_t)blockIdx.x * 8 + wave) * 8;
+            for (int i = 0; i < 4; ++i) o[i] = ts[i];
+            o[4] = rt0; o[5] = rt1; o[6] = ((uint64_t)xcc << 32) | hw;
+        }
     }
 }
 
@@ -454,7 +484,7 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     static_assert(NS >= 2 && NS <= 4, "X ring depth");
     __shared__ __attribute__((aligned(16))) char smem[NS * XB];
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int b = blockIdx.x, xcd = b & 7, qq = nTiles >> 3, rr = nTiles & 7;
     const int t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
     const int m0 = (t / nN) * BM, n0 = (t % nN) * BN;
@@ -695,19 +725,21 @@ int launch_gemm_q_stamped(const DevWeight &W, const uint16_t *X, int32_t M, cons
     const h16 *x = (const h16 *)X;
     const int BN = 256 / wm;
     if (wm == 1) {
+        // stamps == nullptr: the same variant without the stamps (for timing)
+        auto qwd = [&](auto dtag) {
+            constexpr int D = decltype(dtag)::value;
+            if (stamps) dispatch_qw<FMT_Q4_0, 1, D | 0x10>(W, x, M, bias, epi, res, out, s, ResLN(), stamps);
+            else dispatch_qw<FMT_Q4_0, 1, D>(W, x, M, bias, epi, res, out, s, ResLN(), nullptr);
+        };
         switch (diag) {
-        case 1: dispatch_qw<FMT_Q4_0, 1, 0x11>(W, x, M, bias, epi, res, out, s, ResLN(), stamps); break;
-        case 2: dispatch_qw<FMT_Q4_0, 1, 0x12>(W, x, M, bias, epi, res, out, s, ResLN(), stamps); break;
-        case 3: dispatch_qw<FMT_Q4_0, 1, 0x13>(W, x, M, bias, epi, res, out, s, ResLN(), stamps); break;
-        case 4: dispatch_qw<FMT_Q4_0, 1, 0x14>(W, x, M, bias, epi, res, out, s, ResLN(), stamps); break;
-        case 8: dispatch_qw<FMT_Q4_0, 1, 0x18>(W, x, M, bias, epi, res, out, s, ResLN(), stamps); break;
-        case 15: dispatch_qw<FMT_Q4_0, 1, 0x1f>(W, x, M, bias, epi, res, out, s, ResLN(), stamps); break;
-        case 32: dispatch_qw<FMT_Q4_0, 1, 0x30>(W, x, M, bias, epi, res, out, s, ResLN(), stamps); break;
-        case 36: dispatch_qw<FMT_Q4_0, 1, 0x34>(W, x, M, bias, epi, res, out, s, ResLN(), stamps); break;
-        case 64: dispatch_qw<FMT_Q4_0, 1, 0x50>(W, x, M, bias, epi, res, out, s, ResLN(), stamps); break;
-        case 128: dispatch_qw<FMT_Q4_0, 1, 0x90>(W, x, M, bias, epi, res, out, s, ResLN(), stamps); break;
-        case 192: dispatch_qw<FMT_Q4_0, 1, 0xd0>(W, x, M, bias, epi, res, out, s, ResLN(), stamps); break;
-        default: dispatch_qw<FMT_Q4_0, 1, 0x10>(W, x, M, bias, epi, res, out, s, ResLN(), stamps); break;
+        case 1: qwd(std::integral_constant<int, 0x1>()); break;
+        case 2: qwd(std::integral_constant<int, 0x2>()); break;
+        case 3: qwd(std::integral_constant<int, 0x3>()); break;
+        case 4: qwd(std::integral_constant<int, 0x4>()); break;
+        case 8: qwd(std::integral_constant<int, 0x8>()); break;
+        case 15: qwd(std::integral_constant<int, 0xf>()); break;
+        case 256: qwd(std::integral_constant<int, 0x100>()); break;
+        default: qwd(std::integral_constant<int, 0>()); break;
         }
     } else if (wm == 2) {
         dispatch_qw<FMT_Q4_0, 2, 0x10>(W, x, M, bias, epi, res, out, s, ResLN(), stamps);
@@ -758,6 +790,10 @@ void launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, 
 void launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi, const void *res,
                  void *out, hipStream_t s, const ResLN &rln)
 {
+    if (W.layout == 1) {
+        launch_gemm16(W, X, M, bias, epi, res, out, s, rln);
+        return;
+    }
     const h16 *x = (const h16 *)X;
     switch (W.fmt) {
     case FMT_Q4_0: launch_fmt<FMT_Q4_0>(W, x, M, bias, epi, res, out, s, rln); break;

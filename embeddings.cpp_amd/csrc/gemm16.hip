@@ -1,0 +1,407 @@
+// Linear layers on v_mfma_f32_16x16x32_f16 (gfx950), weights in the "lane
+// order" layout (kernels.h, DevWeight::layout == 1).
+//
+// Same contraction and epilogues as gemm.hip -- Y[m][n] = epi(sum_k X[m][k]
+// W[n][k]) -- with the 16x16x32 MFMA: A = 16 features x 32 k (one quant block
+// per feature), B = 32 k x 16 tokens.  The 16x16x32 loop holds a higher clock
+// under load than the 32x32x16 loop at the same cycles per FLOP
+// (MI355X_MICROARCH.md, DVFS give-back item 7), and one A fragment is exactly
+// one quant block, so each lane's scale is a single f16.
+//
+// Workgroup = NW waves, tile BM tokens x 32*NW features; wave w owns features
+// n0 + 32w .. +31 (two A fragments, a = 0/1 for +0 / +16) and all BM tokens
+// (NJ = BM/16 B fragments per k-slice, each feeding two MFMAs).  Weights
+// never touch LDS: each lane loads its own fragment words (16 B q4, 32 B q8,
+// 64 B f16 per K-step, plus 8 B of scales) into a 3-set register ring two
+// K-steps ahead and expands them between MFMAs.  X goes through an NS-stage
+// LDS ring by LDS-DMA with the XOR swizzle on the source address (chunk
+// c ^ ((row>>1)&7)), which keeps the 16x16x32 B-operand row read
+// (ds_read_b128, lanes = 16 rows x 4 chunks) conflict-free.
+//   NW 8, BM 256, NS 3: one workgroup per CU (96 KiB LDS)
+//   NW 4, BM 256, NS 2 / BM 128, NS 4: two per CU (64 KiB each), so one's
+//   epilogue overlaps the other's MFMAs.
+// Epilogue: accumulator pairs of adjacent 16-token groups are exchanged with
+// v_permlane16_swap so each lane owns 8 consecutive features of one token
+// (16-B loads of bias/residual/LN parameters and one 16-B store).
+#include "device_common.h"
+#include "host_common.h"
+#include "kernels.h"
+
+namespace emb {
+
+namespace {
+
+constexpr int ZK = 64;   // K per step (two k-slices of 32)
+
+__device__ __forceinline__ uint4 zload16(const void *p) { return *(const uint4 *)p; }
+__device__ __forceinline__ uint2 zload8(const void *p) { return *(const uint2 *)p; }
+typedef uint32_t zu32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t zu32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void zpin(uint4 &q)
+{
+    zu32x4 v = __builtin_bit_cast(zu32x4, q);
+    asm volatile("" : "+v"(v));
+    q = __builtin_bit_cast(uint4, v);
+}
+__device__ __forceinline__ void zpin(uint2 &q)
+{
+    zu32x2 v = __builtin_bit_cast(zu32x2, q);
+    asm volatile("" : "+v"(v));
+    q = __builtin_bit_cast(uint2, v);
+}
+
+__device__ __forceinline__ h16 zh(uint2 v, int u)   // f16 number u (0..3) of an 8-byte word pair
+{
+    const uint32_t w = u < 2 ? v.x : v.y;
+    return as_h((uint16_t)((u & 1) ? (w >> 16) : (w & 0xffffu)));
+}
+
+// One K-step of one lane's weight words: fragment (a, s) = features +16a,
+// k-slice s (block 2ks+s), index u = 2a + s.
+template <int FMT>
+struct ZRegs;
+
+template <int FMT>
+struct ZRegsQ4 {
+    uint4 q;           // word u: 8 nibbles, element i at bit 4*(i/2) + 16*(i%2)
+    uint2 d, m;        // f16 scale (and min) of fragment u
+    static constexpr int LOADS = FMT == FMT_Q4_1 ? 3 : 2;
+    static constexpr int QB = 16;
+    __device__ void load(const uint8_t *pq, const uint16_t *pd, const uint16_t *pm)
+    {
+        q = zload16(pq);
+        d = zload8(pd);
+        if (FMT == FMT_Q4_1) m = zload8(pm);
+    }
+    __device__ void pin_all() { zpin(q); zpin(d); if (FMT == FMT_Q4_1) zpin(m); }
+    __device__ h16x8 frag(int u) const
+    {
+        const uint32_t w = u == 0 ? q.x : u == 1 ? q.y : u == 2 ? q.z : q.w;
+        const h16 dh = zh(d, u);
+        const h16x2 d2 = {dh, dh};
+        h16x2 m2 = {(h16)0.0f, (h16)0.0f};
+        if (FMT == FMT_Q4_1) { const h16 mh = zh(m, u); m2 = h16x2{mh, mh}; }
+        const h16 o = FMT == FMT_Q4_1 ? (h16)-1024.0f : (h16)-1032.0f;
+        const h16x2 off = {o, o};
+        h16x8 a;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            h16x2 hh = as_h2(and_or_vs(w >> (4 * p), 0x000F000Fu, 0x64006400u)) + off;
+            hh = FMT == FMT_Q4_1 ? hh * d2 + m2 : hh * d2;
+            a[2 * p] = hh[0];
+            a[2 * p + 1] = hh[1];
+        }
+        return a;
+    }
+};
+template <> struct ZRegs<FMT_Q4_0> : ZRegsQ4<FMT_Q4_0> {};
+template <> struct ZRegs<FMT_Q4_1> : ZRegsQ4<FMT_Q4_1> {};
+
+template <>
+struct ZRegs<FMT_Q8_0> {
+    uint4 q0, q1;      // 8 bytes per fragment u at 8u: (q ^ 0x80), order e0 e2 e1 e3 per 4-group
+    uint2 d;
+    static constexpr int LOADS = 3;
+    static constexpr int QB = 32;
+    __device__ void load(const uint8_t *pq, const uint16_t *pd, const uint16_t *)
+    {
+        q0 = zload16(pq);
+        q1 = zload16(pq + 16);
+        d = zload8(pd);
+    }
+    __device__ void pin_all() { zpin(q0); zpin(q1); zpin(d); }
+    __device__ h16x8 frag(int u) const
+    {
+        const uint32_t w0 = u == 0 ? q0.x : u == 1 ? q0.z : u == 2 ? q1.x : q1.z;
+        const uint32_t w1 = u == 0 ? q0.y : u == 1 ? q0.w : u == 2 ? q1.y : q1.w;
+        const h16 dh = zh(d, u);
+        const h16x2 d2 = {dh, dh};
+        const h16x2 off = {(h16)-1152.0f, (h16)-1152.0f};
+        h16x8 a;
+        const h16x2 p0 = (as_h2((w0 & 0x00FF00FFu) | 0x64006400u) + off) * d2;
+        const h16x2 p1 = (as_h2(((w0 >> 8) & 0x00FF00FFu) | 0x64006400u) + off) * d2;
+        const h16x2 p2 = (as_h2((w1 & 0x00FF00FFu) | 0x64006400u) + off) * d2;
+        const h16x2 p3 = (as_h2(((w1 >> 8) & 0x00FF00FFu) | 0x64006400u) + off) * d2;
+        a[0] = p0[0]; a[1] = p0[1]; a[2] = p1[0]; a[3] = p1[1];
+        a[4] = p2[0]; a[5] = p2[1]; a[6] = p3[0]; a[7] = p3[1];
+        return a;
+    }
+};
+
+template <>
+struct ZRegs<FMT_F16> {
+    uint4 q[4];        // fragment u: 8 f16
+    static constexpr int LOADS = 4;
+    static constexpr int QB = 64;
+    __device__ void load(const uint8_t *pq, const uint16_t *, const uint16_t *)
+    {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) q[i] = zload16(pq + 16 * i);
+    }
+    __device__ void pin_all()
+    {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) zpin(q[i]);
+    }
+    __device__ h16x8 frag(int u) const { return __builtin_bit_cast(h16x8, q[u]); }
+};
+
+// v_permlane16_swap_b32 x, y: rows (16 lanes) 1 and 3 of x trade places with rows
+// 0 and 2 of y.  Inline asm: this compiler drops the builtin's second result
+// (it reuses the first -- seen in the emitted code), and the asm needs the
+// VALU-write -> permlane hazard's two wait states (s_nop 1) itself.
+__device__ __forceinline__ void zswap(float &x, float &y)
+{
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+}
+
+template <int FMT, int EPI, int NW, int BM, int NS>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void gemmz_kernel(DevWeight W, const h16 *__restrict__ X,
+                                                               const float *__restrict__ bias,
+                                                               const void *__restrict__ res, void *__restrict__ out,
+                                                               int nN, int nTiles, ResLN rln)
+{
+    constexpr int BN = 32 * NW;
+    constexpr int NJ = BM / 16;                 // 16-token B fragments per k-slice
+    constexpr int XB = BM * ZK * 2;             // bytes per X stage
+    constexpr int XG = XB / (64 * NW * 16);     // LDS-DMA instructions per wave per stage
+    constexpr int QB = ZRegs<FMT>::QB;
+    constexpr int LQ = ZRegs<FMT>::LOADS;
+    constexpr int P = LQ + XG;                  // vector-memory ops issued per K-step per wave
+    static_assert(NS >= 2 && NS <= 4 && XG >= 1, "X ring");
+    __shared__ __attribute__((aligned(16))) char smem[NS * XB];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int b = blockIdx.x, xcd = b & 7, qq = nTiles >> 3, rr = nTiles & 7;
+    const int t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
+    const int m0 = (t / nN) * BM, n0 = (t % nN) * BN;
+    const int K = W.K, N = W.N, KS = K / ZK;
+    const int fr = lane & 15, g = lane >> 4;
+    const int nw = n0 + 32 * wave;              // this wave's first feature
+    const int grp = min(nw, N - 32) >> 5;       // its 32-feature weight group (clamped past N)
+
+    // LDS-DMA sources: instruction i of this wave fills rows 8*XG*wave + 8i + lane/8;
+    // the swizzle ((row>>1)&7) only differs between even and odd i (XG even)
+    static_assert(XG % 2 == 0, "XG even");
+    const h16 *xp[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int r = 8 * XG * wave + 8 * i + (lane >> 3);
+        xp[i] = X + (size_t)(m0 + r) * K + (((lane & 7) ^ ((r >> 1) & 7)) * 8);
+    }
+    const size_t xrow8 = (size_t)16 * K;        // 16 rows: i -> i + 2
+#define EMB_ISSUE_XZ(ks_, stage_)                                                                   \
+    {                                                                                               \
+        char *dst_ = smem + (stage_) * XB + ((8 * XG * wave) << 7);                                 \
+        _Pragma("unroll") for (int i = 0; i < XG; ++i)                                              \
+            glds<16>(xp[i & 1] + (i >> 1) * xrow8 + (ks_) * ZK, dst_ + (i << 10));                  \
+    }
+    const uint8_t *wq = (const uint8_t *)W.qs + ((size_t)grp * 64 + lane) * QB;
+    const uint16_t *wd = W.d + ((size_t)grp * 16 + fr) * 4;
+    const uint16_t *wmn = FMT == FMT_Q4_1 ? W.m + ((size_t)grp * 16 + fr) * 4 : nullptr;
+    const size_t qstep = (size_t)N * 2 * QB, sstep = (size_t)N * 2;
+
+    f32x4 acc[2][NJ];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[a][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    ZRegs<FMT> w0, w1, w2;
+    const int k1 = min(1, KS - 1);
+    w0.load(wq, wd, wmn);
+    EMB_ISSUE_XZ(0, 0)
+    if constexpr (NS == 2) {
+        w1.load(wq + k1 * qstep, wd + k1 * sstep, FMT == FMT_Q4_1 ? wmn + k1 * sstep : nullptr);
+        wait_vmcnt<LQ>();
+    } else if constexpr (NS == 3) {
+        asm volatile("" ::: "memory");
+        w1.load(wq + k1 * qstep, wd + k1 * sstep, FMT == FMT_Q4_1 ? wmn + k1 * sstep : nullptr);
+        asm volatile("" ::: "memory");
+        EMB_ISSUE_XZ(k1, 1)
+        wait_vmcnt<P>();
+    } else {
+        EMB_ISSUE_XZ(k1, 1)
+        asm volatile("" ::: "memory");
+        w1.load(wq + k1 * qstep, wd + k1 * sstep, FMT == FMT_Q4_1 ? wmn + k1 * sstep : nullptr);
+        asm volatile("" ::: "memory");
+        EMB_ISSUE_XZ(min(2, KS - 1), 2)
+        wait_vmcnt<P + XG>();
+    }
+    lds_barrier();
+
+    const int sw = (fr >> 1) & 7;
+    const int rbase = fr << 7;
+    int st = 0;
+
+// One K-step with CUR's weights (see gemm.hip EMB_VSTEP for the wait logic).
+#define EMB_ZSTEP(CUR, NXT2, ks_)                                                                         \
+    {                                                                                                     \
+        const int ksx = (ks_);                                                                            \
+        {                                                                                                 \
+            const int kx = min(ksx + NS - 1, KS - 1), k2 = min(ksx + 2, KS - 1);                          \
+            const int sx = st == 0 ? NS - 1 : st - 1;                                                     \
+            if constexpr (NS == 2) {                                                                      \
+                EMB_ISSUE_XZ(kx, sx)                                                                      \
+                asm volatile("" ::: "memory");                                                            \
+                NXT2.load(wq + k2 * qstep, wd + k2 * sstep, FMT == FMT_Q4_1 ? wmn + k2 * sstep : nullptr); \
+                wait_vmcnt<2 * LQ + XG>();                                                                \
+            } else {                                                                                      \
+                NXT2.load(wq + k2 * qstep, wd + k2 * sstep, FMT == FMT_Q4_1 ? wmn + k2 * sstep : nullptr); \
+                asm volatile("" ::: "memory");                                                            \
+                EMB_ISSUE_XZ(kx, sx)                                                                      \
+                wait_vmcnt<2 * P + (NS == 4 ? XG : 0)>();                                                 \
+            }                                                                                             \
+            CUR.pin_all();                                                                                \
+        }                                                                                                 \
+        const char *xs = smem + st * XB + rbase;                                                          \
+        _Pragma("unroll") for (int s = 0; s < 2; ++s)                                                     \
+        {                                                                                                 \
+            const int cx = ((4 * s + g) ^ sw) << 4;                                                       \
+            const h16x8 a0 = CUR.frag(s), a1 = CUR.frag(2 + s);                                           \
+            _Pragma("unroll") for (int j = 0; j < NJ; ++j)                                                \
+            {                                                                                             \
+                const h16x8 bf = *(const h16x8 *)(xs + (j << 11) + cx);                                   \
+                acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, bf, acc[0][j], 0, 0, 0);           \
+                acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, bf, acc[1][j], 0, 0, 0);           \
+            }                                                                                             \
+        }                                                                                                 \
+        if constexpr (NS == 2) wait_vmcnt<LQ>();                                                          \
+        else if constexpr (NS == 3) wait_vmcnt<P>();                                                      \
+        else wait_vmcnt<P + XG>();                                                                        \
+        lds_barrier();                                                                                    \
+        st = st == NS - 1 ? 0 : st + 1;                                                                   \
+    }
+
+    int ks = 0;
+    for (; ks + 3 <= KS; ks += 3) {
+        EMB_ZSTEP(w0, w2, ks)
+        EMB_ZSTEP(w1, w0, ks + 1)
+        EMB_ZSTEP(w2, w1, ks + 2)
+    }
+    if (ks < KS) {
+        EMB_ZSTEP(w0, w2, ks)
+        if (ks + 1 < KS) EMB_ZSTEP(w1, w0, ks + 1)
+    }
+#undef EMB_ZSTEP
+#undef EMB_ISSUE_XZ
+    wait_vmcnt<0>();
+
+    // ---- epilogue ----
+    // acc[a][j] lane (g, fr): token m0 + 16j + fr, features nw + 16a + 4g + 0..3.
+    // After the permlane16 exchange of (acc[a][j], acc[a][j+1]) the lane holds
+    // token m0 + 16(j + (g&1)) + fr, features nw + 16a + 8(g>>1) + 0..7.
+    if (nw >= N) return;                        // wave-uniform (N % 32 == 0)
+    f32x4 bb[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+        const float *bp = bias + nw + 16 * a + 8 * (g >> 1);
+        bb[a][0] = *(const f32x4 *)bp;
+        bb[a][1] = *(const f32x4 *)(bp + 4);
+    }
+    f32x4 lw[2][2], lb[2][2];
+    if (EPI == EPI_BIAS_RES && rln.stats) {
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+            const int c = nw + 16 * a + 8 * (g >> 1);
+            lw[a][0] = *(const f32x4 *)(rln.w + c);
+            lw[a][1] = *(const f32x4 *)(rln.w + c + 4);
+            lb[a][0] = *(const f32x4 *)(rln.b + c);
+            lb[a][1] = *(const f32x4 *)(rln.b + c + 4);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; j += 2) {
+        const int tok = m0 + 16 * (j + (g & 1)) + fr;
+        float2 stt = {0.f, 1.f};
+        if (EPI == EPI_BIAS_RES && rln.stats) stt = rln.stats[tok];
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                v[e] = acc[a][j][e];
+                v[4 + e] = acc[a][j + 1][e];
+                zswap(v[e], v[4 + e]);
+            }
+            const int c = nw + 16 * a + 8 * (g >> 1);
+            const size_t o = (size_t)tok * N + c;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += bb[a][e >> 2][e & 3];
+            uint4 pk;
+            uint32_t *pw = (uint32_t *)&pk;
+            if constexpr (EPI == EPI_BIAS_RES) {
+                const uint4 r16 = *(const uint4 *)((const h16 *)res + o);
+                const h16x8 rh = __builtin_bit_cast(h16x8, r16);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    float r = (float)rh[e];
+                    if (rln.stats) r = ln_apply(r, stt.x, stt.y, lw[a][e >> 2][e & 3], lb[a][e >> 2][e & 3]);
+                    v[e] += r;
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    pw[e] = __builtin_bit_cast(uint32_t, h16x2{(h16)v[2 * e], (h16)v[2 * e + 1]});
+            } else if constexpr (EPI == EPI_BIAS_GELU_F16) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) pw[e] = gelu2_era(v[2 * e], v[2 * e + 1]);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    pw[e] = __builtin_bit_cast(uint32_t, h16x2{(h16)v[2 * e], (h16)v[2 * e + 1]});
+            }
+            *(uint4 *)((h16 *)out + o) = pk;
+        }
+    }
+}
+
+template <int FMT, int NW, int BM, int NS>
+void dispatch_z(const DevWeight &W, const h16 *x, int M, const float *bias, int epi, const void *res, void *out,
+                hipStream_t s, const ResLN &rln)
+{
+    constexpr int BN = 32 * NW;
+    const int nN = (W.N + BN - 1) / BN, nTiles = (M / BM) * nN;
+    if (epi == EPI_BIAS_F16)
+        gemmz_kernel<FMT, EPI_BIAS_F16, NW, BM, NS><<<nTiles, 64 * NW, 0, s>>>(W, x, bias, res, out, nN, nTiles, rln);
+    else if (epi == EPI_BIAS_GELU_F16)
+        gemmz_kernel<FMT, EPI_BIAS_GELU_F16, NW, BM, NS><<<nTiles, 64 * NW, 0, s>>>(W, x, bias, res, out, nN, nTiles,
+                                                                                   rln);
+    else
+        gemmz_kernel<FMT, EPI_BIAS_RES, NW, BM, NS><<<nTiles, 64 * NW, 0, s>>>(W, x, bias, res, out, nN, nTiles, rln);
+}
+
+template <int FMT>
+void launch_z_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, int32_t epi, const void *res,
+                  void *out, hipStream_t s, const ResLN &rln, int cfg)
+{
+    if (cfg == 0) {
+        // measured (profiles/r01_gemm16_sweep.log): the residual form (N = d) runs
+        // fastest as 128 x 128 tiles two per CU (1536 tiles at bge-base: whole
+        // rounds of 512 slots, where 256 x 256 leaves 384 tiles = 1.5 rounds);
+        // the wide forms as one 256 x 256 workgroup per CU once that fills the chip
+        if (epi != EPI_BIAS_RES && W.N % 256 == 0 && (long)(M / 256) * (W.N / 256) >= 256) cfg = 1;
+        else cfg = 3;
+    }
+    if (cfg == 1) dispatch_z<FMT, 8, 256, 3>(W, x, M, bias, epi, res, out, s, rln);
+    else if (cfg == 2) dispatch_z<FMT, 4, 256, 2>(W, x, M, bias, epi, res, out, s, rln);
+    else dispatch_z<FMT, 4, 128, 4>(W, x, M, bias, epi, res, out, s, rln);
+}
+
+}  // namespace
+
+int g_gemm16_cfg = 0;
+
+void launch_gemm16(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi,
+                   const void *res, void *out, hipStream_t s, const ResLN &rln)
+{
+    const h16 *x = (const h16 *)X;
+    const int cfg = g_gemm16_cfg;
+    switch (W.fmt) {
+    case FMT_Q4_0: launch_z_fmt<FMT_Q4_0>(W, x, M, bias, epi, res, out, s, rln, cfg); break;
+    case FMT_Q4_1: launch_z_fmt<FMT_Q4_1>(W, x, M, bias, epi, res, out, s, rln, cfg); break;
+    case FMT_Q8_0: launch_z_fmt<FMT_Q8_0>(W, x, M, bias, epi, res, out, s, rln, cfg); break;
+    default: launch_z_fmt<FMT_F16>(W, x, M, bias, epi, res, out, s, rln, cfg); break;
+    }
+}
+
+}  // namespace emb

@@ -38,6 +38,7 @@ struct DevWeight {
     const void *qs = nullptr;       // values / nibbles / int8
     const uint16_t *d = nullptr;    // f16 scales [K/64][N][2]
     const uint16_t *m = nullptr;    // f16 mins (q4_1)
+    int32_t layout = 0;             // 0: fragment order of gemm.hip, 1: lane order of gemm16.hip
 };
 
 struct DevTable {
@@ -73,6 +74,20 @@ __host__ __device__ __forceinline__ float ln_apply(float v, float mean, float sc
 // out (in place, element-wise).
 void launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi,
                  const void *res, void *out, hipStream_t s, const ResLN &rln = ResLN());
+
+// Weight layout 1 (gemm16.hip, v_mfma_f32_16x16x32_f16): per K-step (64 k =
+// blocks 2ks, 2ks+1) and 32-feature group, 64 lane records; lane l = 16g + f
+// holds fragments u = 2a + s (feature 32grp + 16a + f, block 2ks + s,
+// elements 8g .. 8g+7): q4 16 B (word u, element i at bit 4(i/2) + 16(i%2)),
+// q8 32 B (8 B per u, (q ^ 0x80) in order e0 e2 e1 e3 per 4-group), f16 64 B;
+// d (and m) f16 [ks][grp][f][u].  N % 32 == 0.
+void launch_gemm16(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi,
+                   const void *res, void *out, hipStream_t s, const ResLN &rln);
+// Benches/tests: gemm16 tile config (0 = heuristic, 1 = 8 waves 256x256, 2 = 4 waves 256x128,
+// 3 = 4 waves 128x128).
+extern int g_gemm16_cfg;
+// Layout the engine repacks linear weights into (BERT_GEMM_LAYOUT overrides).
+extern int g_weight_layout;
 
 // Tests only: force the GEMM tile shape (128 / 256; 0 = heuristic).
 extern int g_force_bn;

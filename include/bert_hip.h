@@ -71,7 +71,10 @@ BERT_API int32_t bertx_convert_hf(const char *dir_model, const char *fname_out, 
  * (N rows of K elements in format `fmt` = 0,1,2,3,8).  x: f16 bits [M][K].
  * epi: 0 = +bias -> f16, 1 = +bias, GELU -> f16, 2 = +bias +res -> f16 (res f16 [M][N],
  * the residual-stream form; sum in f32).
- * tile_n: 0 = the production tile choice, 128 / 256 = force that tile width.
+ * tile_n: 0 = the production kernel and weight layout; 128 / 256 = gemm.hip
+ * (32x32x16 MFMA, weight layout 0) with that tile width; 0x1000 | c = gemm16.hip
+ * (16x16x32 MFMA, weight layout 1) with tile config c (0 heuristic, 1 = 8 waves
+ * 256x256, 2 = 4 waves 256x128, 3 = 4 waves 128x128).
  */
 BERT_API int32_t bertx_test_gemm(int32_t fmt, int32_t N, int32_t K, const void *w_rows,
                                  const float *bias, int32_t M, const uint16_t *x,
@@ -79,12 +82,14 @@ BERT_API int32_t bertx_test_gemm(int32_t fmt, int32_t N, int32_t K, const void *
 
 /*
  * GEMM micro-benchmark on random operands (device 0): average device time of
- * `iters` launches of the production GEMM for fmt / N / K / M / epi (tile_n 0 =
- * production choice).  ablate: -1 = production kernels; -2 = the one-workgroup-
- * per-CU kernel (gemmqw) for every form; -3 - d (q4_0 only) = one extra launch of
- * a diagnostic gemmqw build with per-wave s_memtime phase stamps (printed to
- * stderr) and ablation bits d (1 no dequant, 2 no B reads, 4 no K-loop barrier,
- * 8 no MFMA, 32 sched-group pipelined).
+ * `iters` launches of the GEMM for fmt / N / K / M / epi.  tile_n: 0 / 128 / 256 =
+ * gemm.hip (layout 0) heuristic / tile width; 0x1000 | c = gemm16.hip config c (as
+ * bertx_test_gemm).  ablate: -1 = production kernels; -2 = the one-workgroup-
+ * per-CU kernel (gemmqw) for every form; -3 - d (q4_0, tile_n 0 or 256) = a
+ * diagnostic gemmqw build: one launch with per-wave s_memtime phase stamps
+ * (printed to stderr), then the timed launches of the same build without stamps;
+ * d = ablation bits (1 no dequant, 2 no B reads, 4 no K-loop barrier, 8 no MFMA)
+ * or 256 (B reads software-pipelined two ahead).
  */
 BERT_API int32_t bertx_bench_gemm(int32_t fmt, int32_t N, int32_t K, int32_t M, int32_t epi, int32_t tile_n,
                                   int32_t ablate, int32_t iters, float *avg_us);

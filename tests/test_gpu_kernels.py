@@ -52,10 +52,14 @@ def run_gemm(lib, fmt, W, bias, X, epi, res=None, tile_n=0):
 @pytest.mark.parametrize("fmt", sorted(FMTS))
 @pytest.mark.parametrize("epi", [0, 1, 2])
 @pytest.mark.parametrize("shape", [(192, 256, 300, 0), (768, 768, 512, 0), (512, 192, 700, 256),
-                                   (256, 3072, 256, 128)])
+                                   (256, 3072, 256, 128),
+                                   # gemm16 (layout 1) configs: 0x1000 | 1 (8 waves 256x256),
+                                   # 2 (4 waves 256x128), 3 (4 waves 128x128)
+                                   (768, 768, 512, 0x1001), (2304, 768, 768, 0x1002), (448, 192, 700, 0x1003),
+                                   (256, 3072, 256, 0x1001)])
 def test_gemm_matches_numpy(lib, fmt, epi, shape):
     N, K, M, tile_n = shape
-    if tile_n == 256 and epi == 2:
+    if tile_n == 256 and epi == 2:   # gemm.hip's 256-wide tile has no residual form
         pytest.skip("the residual epilogue runs 128 wide")
     rng = np.random.default_rng(fmt * 10 + epi)
     W = rng.standard_normal((N, K)).astype(np.float32) * 0.05
