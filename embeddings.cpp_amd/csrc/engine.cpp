@@ -683,6 +683,22 @@ extern "C" int32_t bertx_bench_gemm(int32_t fmt, int32_t N, int32_t K, int32_t M
     HIP_RC(hipMalloc((void **)&dr, (size_t)Mp * N * 4));
     HIP_RC(hipMemset(dr, 0, (size_t)Mp * N * 4));
     HIP_RC(hipMalloc((void **)&dout, (size_t)Mp * N * 4));
+    // the residual form as the forward runs it: LN of the residual recomputed from
+    // per-row (mean, 1/sigma) and gamma/beta (kernels.h ResLN)
+    char *dst_ln = nullptr, *dwb = nullptr;
+    ResLN rln;
+    if (epi == EPI_BIAS_RES) {
+        std::vector<float> hs((size_t)Mp * 2), hwb((size_t)N * 2);
+        for (size_t i = 0; i < hs.size(); i += 2) { hs[i] = 0.01f; hs[i + 1] = 1.0f + (rnd() >> 24) / 2560.0f; }
+        for (size_t i = 0; i < hwb.size(); ++i) hwb[i] = i < (size_t)N ? 1.0f : 0.0f;
+        HIP_RC(hipMalloc((void **)&dst_ln, hs.size() * 4));
+        HIP_RC(hipMemcpy(dst_ln, hs.data(), hs.size() * 4, hipMemcpyHostToDevice));
+        HIP_RC(hipMalloc((void **)&dwb, hwb.size() * 4));
+        HIP_RC(hipMemcpy(dwb, hwb.data(), hwb.size() * 4, hipMemcpyHostToDevice));
+        rln.stats = (const float2 *)dst_ln;
+        rln.w = (const float *)dwb;
+        rln.b = (const float *)dwb + N;
+    }
     DevWeight W;
     W.fmt = fdev; W.N = N; W.K = K;
     W.qs = dq; W.d = (const uint16_t *)dd; W.m = (const uint16_t *)dd;
@@ -692,7 +708,7 @@ extern "C" int32_t bertx_bench_gemm(int32_t fmt, int32_t N, int32_t K, int32_t M
         g_force_bn = W.layout ? 0 : tile_n;
         g_gemm16_cfg = W.layout ? (tile_n & 0xff) : 0;
         g_gemm_variant = ablate == -2 ? 2 : 0;   // -2: gemmqw everywhere
-        launch_gemm(W, (const uint16_t *)dx, Mp, (const float *)db, epi, (const void *)dr, dout, nullptr);
+        launch_gemm(W, (const uint16_t *)dx, Mp, (const float *)db, epi, (const void *)dr, dout, nullptr, rln);
         g_force_bn = 0;
         g_gemm16_cfg = 0;
         g_gemm_variant = 0;
@@ -783,7 +799,7 @@ extern "C" int32_t bertx_bench_gemm(int32_t fmt, int32_t N, int32_t K, int32_t M
     *avg_us = ms * 1000.0f / (float)iters;
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
-    for (char *p : {dq, dd, dx, db, dr, dout}) (void)hipFree(p);
+    for (char *p : {dq, dd, dx, db, dr, dout, dst_ln, dwb}) if (p) (void)hipFree(p);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

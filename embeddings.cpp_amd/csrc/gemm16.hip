@@ -310,11 +310,26 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void gemmz_kernel(DevWeight W, con
             lb[a][1] = *(const f32x4 *)(rln.b + c + 4);
         }
     }
+    // residual form: every residual row chunk and LN statistic of up to 8 token
+    // pairs in flight before the first use (one latency, not one per pair)
+    constexpr int JC = NJ < 16 ? NJ : 8;        // token groups per prefetch chunk
 #pragma unroll
-    for (int j = 0; j < NJ; j += 2) {
+    for (int jc = 0; jc < NJ; jc += JC) {
+    uint4 rr[JC / 2][2];
+    float2 sts[JC / 2];
+    if constexpr (EPI == EPI_BIAS_RES) {
+#pragma unroll
+        for (int jp = 0; jp < JC / 2; ++jp) {
+            const int tok = m0 + 16 * (jc + 2 * jp + (g & 1)) + fr;
+            sts[jp] = rln.stats ? rln.stats[tok] : float2{0.f, 1.f};
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+                rr[jp][a] = *(const uint4 *)((const h16 *)res + (size_t)tok * N + nw + 16 * a + 8 * (g >> 1));
+        }
+    }
+#pragma unroll
+    for (int j = jc; j < jc + JC; j += 2) {
         const int tok = m0 + 16 * (j + (g & 1)) + fr;
-        float2 stt = {0.f, 1.f};
-        if (EPI == EPI_BIAS_RES && rln.stats) stt = rln.stats[tok];
 #pragma unroll
         for (int a = 0; a < 2; ++a) {
             float v[8];
@@ -331,8 +346,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void gemmz_kernel(DevWeight W, con
             uint4 pk;
             uint32_t *pw = (uint32_t *)&pk;
             if constexpr (EPI == EPI_BIAS_RES) {
-                const uint4 r16 = *(const uint4 *)((const h16 *)res + o);
-                const h16x8 rh = __builtin_bit_cast(h16x8, r16);
+                const h16x8 rh = __builtin_bit_cast(h16x8, rr[(j - jc) >> 1][a]);
+                const float2 stt = sts[(j - jc) >> 1];
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
                     float r = (float)rh[e];
@@ -352,6 +367,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void gemmz_kernel(DevWeight W, con
             }
             *(uint4 *)((h16 *)out + o) = pk;
         }
+    }
     }
 }
 
