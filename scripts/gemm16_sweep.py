@@ -15,7 +15,8 @@ L = bertpy.load_lib()
 M = int(os.environ.get("SWEEP_M", "32768"))
 cases = [("qkv", 2, 2304, 768, 0), ("attn_out", 2, 768, 768, 2), ("ffn_up", 2, 3072, 768, 1),
          ("ffn_down", 2, 768, 3072, 2), ("ffn_up_q8", 8, 3072, 768, 1), ("ffn_up_q41", 3, 3072, 768, 1),
-         ("ffn_up_f16", 1, 3072, 768, 1)]
+         ("ffn_up_f16", 1, 3072, 768, 1), ("qkv_f16", 1, 2304, 768, 0), ("attn_out_f16", 1, 768, 768, 2),
+         ("ffn_down_f16", 1, 768, 3072, 2)]
 want = os.environ.get("SWEEP_CASES")
 if want:
     cases = [c for c in cases if c[0] in want.split(",")]

@@ -37,7 +37,7 @@ def classify(rows):
     out, res_i = [], 0
     for r in rows:
         k = r["Kernel_Name"]
-        m = re.search(r"gemmq[vw]?_kernelILi(\d+)ELi(\d+)E", k)
+        m = re.search(r"gemm[qvwz]*_kernelILi(\d+)ELi(\d+)E", k)
         if m:
             epi = int(m.group(2))
             if epi == 0:
@@ -47,7 +47,7 @@ def classify(rows):
             else:
                 c = "gemm_attn_out" if res_i % 2 == 0 else "gemm_ffn_down"
                 res_i += 1
-        elif "attention_kernel" in k:
+        elif "attention" in k:
             c = "attention"
         elif "layernorm_kernel" in k:
             c = "layernorm"
