@@ -73,6 +73,8 @@ def load_lib(path=None):
     L.bertx_convert_hf.restype = c_i32
     L.bertx_convert_hf.argtypes = [ctypes.c_char_p, ctypes.c_char_p, c_i32]
     L.bertx_test_gemm.restype = c_i32
+    L.bertx_test_attention.restype = c_i32
+    L.bertx_test_attention.argtypes = [vp, vp, c_i32, c_i32, c_i32, c_i32, vp]
     L.bertx_test_gemm.argtypes = [c_i32, c_i32, c_i32, vp, c_f32p, c_i32, vp, c_i32, vp, vp, c_i32]
     L.bertx_bench_gemm.restype = c_i32
     L.bertx_bench_gemm.argtypes = [c_i32] * 8 + [c_f32p]

@@ -164,7 +164,6 @@ __global__ __launch_bounds__(256) void attention_kernel(const h16 *__restrict__ 
 template <int CH, int VAR = 0>
 __device__ __forceinline__ int kswz(int row)
 {
-    if constexpr (VAR == 1) return row & (CH - 1);   // A/B only: the first (2-way conflicted) form
     return CH == 8 ? ((row >> 1) & 7) : ((row >> 2) & 3);
 }
 
@@ -309,6 +308,301 @@ __global__ __launch_bounds__(1024) void attention_lds_kernel(const h16 *__restri
     }
 }
 
+// ---------------------------------------------------------------------------
+// attention_lds2: the attention_lds structure (one workgroup per (sentence,
+// head), whole K/V in LDS, 16 waves x 32 queries, S^T = K Q^T with the query
+// on the lane) with the softmax VALU cut to the exp, the row sum and the f16
+// packing per score, and the K/V load overlapped with the first blocks:
+//  * fixed offset: each query keeps an f16 offset c (the max of its first
+//    block) and S - c comes out of the MFMA itself -- one extra MFMA per
+//    32 keys multiplies a ones-column of K by a (-c)-row of Q.  softmax(S) =
+//    exp2(S - c) / sum exp2(S - c) for any c, so the result is the function
+//    of the running-max form.  No max is taken per block: a block whose
+//    32-key partial row sum exceeds 2^ATT_SUMX (so some P may leave the safe
+//    f16 range) is recomputed after moving c to the row max and rescaling O
+//    and l -- rare, and it keeps every P <= 2^ATT_SUMX.
+//  * the row sum stays per 32-lane half (no cross-lane op per block); the
+//    halves are combined once, by v_permlane32_swap, at the end.
+//  * LDS reads at base + immediate offsets (the swizzles of both images are
+//    lane constants for 16-row-aligned blocks): six address adds per block.
+//  * K arrives first: the first block's Q K^T and softmax overlap V's DMA.
+// ---------------------------------------------------------------------------
+constexpr int ATT_SUMX = 12;
+
+__device__ __forceinline__ void swap32(float &a, float &b)
+{
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+}
+// x over both 32-lane halves: lanes l and l ^ 32 combined
+__device__ __forceinline__ float halves_max(float x)
+{
+    float a = x, b = x;
+    swap32(a, b);
+    return fmaxf(a, b);
+}
+__device__ __forceinline__ float halves_sum(float x)
+{
+    float a = x, b = x;
+    swap32(a, b);
+    return a + b;
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt_upto(int n)   // s_waitcnt vmcnt(min(n, N)), n >= 0
+{
+    if constexpr (N == 0) wait_vmcnt<0>();
+    else {
+        if (n >= N) wait_vmcnt<N>();
+        else wait_vmcnt_upto<N - 1>(n);
+    }
+}
+
+// ABL (A/B diagnostics only): 1 = loads only, 2 = no K/V loads (compute on stale LDS),
+// 3 = stagger (waves w >= 4, 8, 12 start 320 cycles apart), 4 = s_setprio 1 around
+// the MFMA sections, 5 = K and V interleaved with one wait + stagger
+template <int ABL = 0>
+__global__ __launch_bounds__(1024) void attention_lds2_kernel(const h16 *__restrict__ qkv,
+                                                              const int32_t *__restrict__ cu, int d, int nh,
+                                                              float sl2, h16 *__restrict__ out)
+{
+    constexpr int DH = 64, RB = DH * 2, CH = RB / 16, LMAX = ATT_LDS_MAX;
+    __shared__ __attribute__((aligned(16))) char smem[2 * LMAX * RB];
+    char *Kl = smem;
+    const int h = blockIdx.x % nh, b = blockIdx.x / nh;
+    const int start = cu[b], len = cu[b + 1] - start;
+    if (len <= 0) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int hi = lane >> 5, lq = lane & 31;
+    const int ld = 3 * d;
+    const int nrows = (len + 63) & ~63;
+    const int q0 = 32 * w, q = q0 + lq;
+    const bool active = q0 < len && ABL != 1;             // wave-uniform
+
+    // Q rows first (older than the DMA, so every stage wait covers them)
+    h16x8 qf[DH / 16];
+    {
+        const h16 *qrow = qkv + (size_t)(start + min(q, len - 1)) * ld + h * DH;
+#pragma unroll
+        for (int s = 0; s < DH / 16; ++s) qf[s] = *(const h16x8 *)(qrow + 16 * s + 8 * hi);
+    }
+    // K and V -> LDS, 64 chunks of 16 B per wave-instruction; piece i = rows
+    // 8i .. 8i+7, wave w issues pieces w, w + 16, ... (stage j = pieces 16j ..
+    // 16j + 15 = rows 128j .. 128j + 127).  K swizzled by (row >> 1) & 7, V by
+    // ((row >> 1) & 1) << 2, via the source address; rows past the end are
+    // finite copies (masked / P = 0).
+    // ABL 5: pieces issued K, V interleaved, one wait; otherwise every K piece
+    // first, then every V piece: the first block's Q K^T and softmax run under V's DMA
+    constexpr bool SPLIT = ABL != 5;
+    int J = 0;                                            // this wave's pieces
+    {
+        const int ninstr = nrows * CH / 64;
+        const h16 *kbase = qkv + (size_t)start * ld + d + h * DH;
+        const h16 *vbase = kbase + d;
+        for (int i = w; i < ninstr; i += 16, ++J) {
+            const int g = i * 64 + lane, row = g / CH, pc = g % CH;
+            const size_t so = (size_t)min(row, len - 1) * ld;
+            if (ABL != 2) {
+                glds<16>(kbase + so + (pc ^ ((row >> 1) & 7)) * 8, Kl + i * 1024);
+                if (!SPLIT) glds<16>(vbase + so + (pc ^ (((row >> 1) & 1) << 2)) * 8, Kl + LMAX * RB + i * 1024);
+            }
+        }
+        if (SPLIT && ABL != 2)
+            for (int i = w; i < ninstr; i += 16) {
+                const int g = i * 64 + lane, row = g / CH, pc = g % CH;
+                const size_t so = (size_t)min(row, len - 1) * ld;
+                glds<16>(vbase + so + (pc ^ (((row >> 1) & 1) << 2)) * 8, Kl + LMAX * RB + i * 1024);
+            }
+    }
+    auto k_landed = [&]() {                               // every wave's K (and Q) pieces
+        if (SPLIT) wait_vmcnt_upto<4>(J);
+        else wait_vmcnt<0>();
+        __syncthreads();
+    };
+    auto v_landed = [&]() {                               // every wave's V pieces
+        if (SPLIT) {
+            wait_vmcnt<0>();
+            __syncthreads();
+        }
+    };
+    auto prio = [&](int p) {
+        if (ABL == 4) {
+            if (p) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
+    };
+
+    // lane-constant LDS offsets (blocks are 64-row aligned)
+    int koff[DH / 16];
+#pragma unroll
+    for (int st = 0; st < DH / 16; ++st) koff[st] = lq * RB + (((2 * st + hi) ^ ((lq >> 1) & 7)) << 4);
+    const int gi = lane & 15, gq = gi >> 2, gp = gi & 3, gg = lane >> 4;
+    const int vsw = ((gq >> 1) & 1) << 2;
+    int voff[DH / 32];
+#pragma unroll
+    for (int t = 0; t < DH / 32; ++t) {
+        const int ch = 4 * t + 2 * (gg & 1) + (gp >> 1);
+        voff[t] = (4 * (gg >> 1) + gq) * RB + ((ch ^ vsw) << 4) + 8 * (gp & 1);
+    }
+    const h16 one = (h16)1.0f, zero = (h16)0.0f;
+    const h16x8 abias = {hi ? zero : one, zero, zero, zero, zero, zero, zero, zero};
+    h16x8 bbias = {zero, zero, zero, zero, zero, zero, zero, zero};
+
+    f32x16 o[DH / 32];
+#pragma unroll
+    for (int t = 0; t < DH / 32; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[t][r] = 0.f;
+    float c = 0.f, l = 0.f;                               // offset (f16-exact), this half's row sum
+    f32x16 s[2];
+
+    // per-block LDS bases pinned in VGPRs (the asm hides their constant parts,
+    // so every read is base + a 16-bit immediate offset)
+    auto qk = [&](int kb, bool bias) {
+        prio(1);
+        int kbo[DH / 16];
+#pragma unroll
+        for (int st = 0; st < DH / 16; ++st) {
+            kbo[st] = koff[st] + kb * RB;
+            asm volatile("" : "+v"(kbo[st]));
+        }
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) {
+            if (bias) {
+                s[kh] = __builtin_amdgcn_mfma_f32_32x32x16_f16(abias, bbias, f32x16{}, 0, 0, 0);
+            } else {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) s[kh][r] = 0.f;
+            }
+#pragma unroll
+            for (int st = 0; st < DH / 16; ++st) {
+                const h16x8 a = *(const h16x8 *)(Kl + kbo[st] + kh * 32 * RB);
+                s[kh] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, qf[st], s[kh], 0, 0, 0);
+            }
+        }
+        prio(0);
+        if (kb + 64 > len) {
+#pragma unroll
+            for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int key = kb + 32 * kh + (r & 3) + 8 * (r >> 2) + 4 * hi;
+                    if (key >= len) s[kh][r] = -INFINITY;
+                }
+        }
+    };
+    auto row_max = [&]() {                                // over both halves
+        float mx = s[0][0];
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+            for (int r = (kh ? 0 : 1); r < 16; ++r) mx = fmaxf(mx, s[kh][r]);
+        return halves_max(mx);
+    };
+    auto shift_by = [&](float sh) {                       // scores -= sh
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[kh][r] -= sh;
+    };
+    auto expsum = [&]() {                                 // s <- exp2(s); this half's sum
+        float rs = 0.f;
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float p = __builtin_amdgcn_exp2f(s[kh][r]);
+                s[kh][r] = p;
+                rs += p;
+            }
+        return rs;
+    };
+    auto pv = [&](int kb) {
+        prio(1);
+        int vbo[DH / 32];
+#pragma unroll
+        for (int t = 0; t < DH / 32; ++t) {
+            vbo[t] = voff[t] + kb * RB + LMAX * RB;
+            asm volatile("" : "+v"(vbo[t]));
+        }
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) {
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                h16x8 bp;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) bp[j] = (h16)s[kh][8 * s2 + j];
+#pragma unroll
+                for (int t = 0; t < DH / 32; ++t) {
+                    const char *va = smem + vbo[t] + (32 * kh + 16 * s2) * RB;
+                    const h16x4 lo = lds_read_tr16(va);
+                    const h16x4 up = lds_read_tr16(va + 8 * RB);
+                    const h16x8 a = {lo[0], lo[1], lo[2], lo[3], up[0], up[1], up[2], up[3]};
+                    o[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bp, o[t], 0, 0, 0);
+                }
+            }
+        }
+        prio(0);
+    };
+
+    k_landed();
+    if (ABL == 3 || ABL == 5) {
+        if (w >= 4) __builtin_amdgcn_s_sleep(5);
+        if (w >= 8) __builtin_amdgcn_s_sleep(5);
+        if (w >= 12) __builtin_amdgcn_s_sleep(5);
+    }
+    if (active) {
+        const h16 s16 = (h16)sl2;
+        const h16x8 sc = {s16, s16, s16, s16, s16, s16, s16, s16};
+#pragma unroll
+        for (int st = 0; st < DH / 16; ++st) qf[st] *= sc;
+        // first block: the offset is its row max (f16-rounded)
+        qk(0, false);
+        c = (float)(h16)row_max();
+        shift_by(c);
+        bbias[0] = hi ? zero : (h16)(-c);
+        l = expsum();
+    }
+    v_landed();
+    if (!active) return;                                  // no barrier follows
+    pv(0);
+    for (int kb = 64; kb < nrows; kb += 64) {
+        qk(kb, true);                                     // S - c
+        float rs = expsum();
+        if (__builtin_amdgcn_ballot_w64(rs > (float)(1 << ATT_SUMX))) {
+            // rare: move c to the row max, rescale, redo the block
+            qk(kb, true);
+            const float m = row_max();
+            const float sh = m > 0.f ? (float)(h16)(c + m) - c : 0.f;
+            const float alpha = __builtin_amdgcn_exp2f(-sh);
+            shift_by(sh);
+            c += sh;
+            bbias[0] = hi ? zero : (h16)(-c);
+            l *= alpha;
+#pragma unroll
+            for (int t = 0; t < DH / 32; ++t)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+            rs = expsum();
+        }
+        l += rs;
+        pv(kb);
+    }
+
+    const float inv = 1.0f / halves_sum(l);
+    if (q < len) {
+        h16 *orow = out + (size_t)(start + q) * d + h * DH;
+#pragma unroll
+        for (int t = 0; t < DH / 32; ++t)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                h16x4 v;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = (h16)(o[t][4 * g + e] * inv);
+                *(h16x4 *)(orow + 32 * t + 8 * g + 4 * hi) = v;
+            }
+    }
+}
+
 int g_att_variant = 0;   // benches only (bertx_bench_attention)
 
 void launch_attention(const uint16_t *qkv, const int32_t *cu, int32_t n_seqs, int32_t max_len, int32_t n_head,
@@ -319,10 +613,19 @@ void launch_attention(const uint16_t *qkv, const int32_t *cu, int32_t n_seqs, in
     if (max_len <= ATT_LDS_MAX && (dh == 64 || dh == 32)) {
         const dim3 g(n_seqs * n_head), blk(1024);
         if (dh == 64) {
-            if (g_att_variant == 1)
-                attention_lds_kernel<64, 1><<<g, blk, 0, s>>>((const h16 *)qkv, cu, d, n_head, sl2, (h16 *)out);
-            else
-                attention_lds_kernel<64, 0><<<g, blk, 0, s>>>((const h16 *)qkv, cu, d, n_head, sl2, (h16 *)out);
+            // 0: production (attention_lds2, MFMA sections at s_setprio 1); 1: the
+            // previous attention_lds; 2..6: attention_lds2 A/B builds (ABL 0, 1, 2, 3, 5)
+            decltype(&attention_lds2_kernel<0>) k = attention_lds2_kernel<4>;
+            switch (g_att_variant) {
+            case 1: k = attention_lds_kernel<64, 0>; break;
+            case 2: k = attention_lds2_kernel<0>; break;
+            case 3: k = attention_lds2_kernel<1>; break;
+            case 4: k = attention_lds2_kernel<2>; break;
+            case 5: k = attention_lds2_kernel<3>; break;
+            case 6: k = attention_lds2_kernel<5>; break;
+            default: break;
+            }
+            k<<<g, blk, 0, s>>>((const h16 *)qkv, cu, d, n_head, sl2, (h16 *)out);
         } else {
             attention_lds_kernel<32, 0><<<g, blk, 0, s>>>((const h16 *)qkv, cu, d, n_head, sl2, (h16 *)out);
         }

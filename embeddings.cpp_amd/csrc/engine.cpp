@@ -845,3 +845,35 @@ extern "C" int32_t bertx_bench_attention(int32_t n_seqs, int32_t len, int32_t n_
     for (void *p : {(void *)dq, (void *)dcu, (void *)dout}) (void)hipFree(p);
     return 0;
 }
+
+extern "C" int32_t bertx_test_attention(const uint16_t *qkv, const int32_t *cu, int32_t n_seqs, int32_t n_head,
+                                        int32_t d, int32_t variant, uint16_t *out)
+{
+    using namespace emb;
+    if (n_seqs <= 0 || n_head <= 0 || d % n_head || hip_device_count() == 0) return -1;
+    const int dh = d / n_head;
+    if (dh != 64 && dh != 32) return -1;
+    int max_len = 0;
+    for (int i = 0; i < n_seqs; ++i) {
+        if (cu[i + 1] < cu[i]) return -1;
+        max_len = std::max(max_len, cu[i + 1] - cu[i]);
+    }
+    const size_t T = (size_t)cu[n_seqs];
+    uint16_t *dq = nullptr, *dout = nullptr;
+    int32_t *dcu = nullptr;
+    HIP_RC(hipSetDevice(0));
+    HIP_RC(hipMalloc((void **)&dq, (T + 64) * 3 * d * 2));
+    HIP_RC(hipMemset(dq, 0, (T + 64) * 3 * d * 2));
+    HIP_RC(hipMemcpy(dq, qkv, T * 3 * d * 2, hipMemcpyHostToDevice));
+    HIP_RC(hipMalloc((void **)&dcu, ((size_t)n_seqs + 1) * 4));
+    HIP_RC(hipMemcpy(dcu, cu, ((size_t)n_seqs + 1) * 4, hipMemcpyHostToDevice));
+    HIP_RC(hipMalloc((void **)&dout, (T + 64) * d * 2));
+    g_att_variant = variant;
+    // variant -1: the streaming kernel, reached by claiming a length past the LDS form
+    launch_attention(dq, dcu, n_seqs, variant == -1 ? ATT_LDS_MAX + 1 : max_len, n_head, d, dout, nullptr);
+    g_att_variant = 0;
+    HIP_RC(hipDeviceSynchronize());
+    HIP_RC(hipMemcpy(out, dout, T * d * 2, hipMemcpyDeviceToHost));
+    for (void *p : {(void *)dq, (void *)dcu, (void *)dout}) (void)hipFree(p);
+    return 0;
+}

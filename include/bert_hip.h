@@ -97,10 +97,21 @@ BERT_API int32_t bertx_bench_gemm(int32_t fmt, int32_t N, int32_t K, int32_t M, 
 /*
  * Attention micro-benchmark on random operands (device 0): average device time
  * of `iters` launches for n_seqs sentences of `len` tokens, n_head heads of size
- * dh; variant 0 = production kernel (others: A/B builds, see attention.hip).
+ * dh; variant 0 = production kernel, 1 = the previous one, others: A/B builds
+ * (launch_attention in attention.hip).
  */
 BERT_API int32_t bertx_bench_attention(int32_t n_seqs, int32_t len, int32_t n_head, int32_t dh, int32_t variant,
                                        int32_t iters, float *avg_us);
+
+/*
+ * Attention parity hook (host buffers, device 0): qkv f16 bits [T][3d] as the
+ * QKV GEMM writes it (packed tokens of n_seqs sentences, cu[n_seqs + 1] the
+ * token offsets), out f16 [T][d] = per (sentence, head) softmax(Q K^T / sqrt(dh)) V
+ * over the sentence's own keys (bert.cpp:1018-1036).  variant as
+ * bertx_bench_attention; -1 = the streaming kernel (sentences > 512).
+ */
+BERT_API int32_t bertx_test_attention(const uint16_t *qkv, const int32_t *cu, int32_t n_seqs, int32_t n_head,
+                                      int32_t d, int32_t variant, uint16_t *out);
 
 BERT_API const char *bertx_version(void);
 

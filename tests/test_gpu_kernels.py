@@ -88,3 +88,44 @@ def test_gemm_matches_numpy(lib, fmt, epi, shape):
     exact = xh.astype(np.float64) @ deq.astype(np.float64).T + bias
     if epi == 0:
         assert np.abs(got - exact).max() <= 5e-3 * np.abs(exact).max()
+
+
+def attention_ref(qkv, cu, n_head, d):
+    """f64 softmax(Q K^T / sqrt(dh)) V per (sentence, head) on the f16 inputs (bert.cpp:1018-1036)."""
+    dh = d // n_head
+    q, k, v = (qkv[:, i * d:(i + 1) * d].astype(np.float64) for i in range(3))
+    out = np.zeros((qkv.shape[0], d))
+    for b in range(len(cu) - 1):
+        s0, s1 = cu[b], cu[b + 1]
+        for h in range(n_head):
+            c = slice(h * dh, (h + 1) * dh)
+            sc = q[s0:s1, c] @ k[s0:s1, c].T / np.sqrt(dh)
+            p = np.exp(sc - sc.max(axis=1, keepdims=True))
+            out[s0:s1, c] = (p / p.sum(axis=1, keepdims=True)) @ v[s0:s1, c]
+    return out
+
+
+@pytest.mark.parametrize("variant,dh", [(0, 64), (1, 64), (2, 64), (6, 64), (-1, 64), (0, 32), (-1, 32)])
+def test_attention_matches_numpy(lib, variant, dh):
+    """Ragged sentences (1 .. 512 tokens, block edges), one with sharp scores whose row
+    maximum moves late (exercises the deferred-max rescale of variant 2)."""
+    n_head = 4
+    d = n_head * dh
+    lens = [1, 5, 63, 64, 65, 200, 512, 130]
+    cu = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    T = int(cu[-1])
+    rng = np.random.default_rng(dh + 3)
+    qkv = rng.standard_normal((T, 3 * d)).astype(np.float32)
+    s0, s1 = cu[7], cu[8]                 # sentence 7: large Q, and keys that grow along the sentence
+    qkv[s0:s1, :d] *= 4.0
+    qkv[s0:s1, d:2 * d] *= np.linspace(0.2, 3.0, s1 - s0)[:, None]
+    qkv = qkv.astype(np.float16)
+    out = np.zeros((T, d), np.float16)
+    rc = lib.bertx_test_attention(qkv.ctypes.data, cu.ctypes.data, len(lens), n_head, d, variant, out.ctypes.data)
+    assert rc == 0
+    ref = attention_ref(qkv, cu, n_head, d)
+    got = out.astype(np.float64)
+    assert np.isfinite(got).all()
+    err = np.abs(got - ref).max()
+    # Q pre-scaled in f16, P rounded to f16 for the MFMA, output f16
+    assert err < 6e-3 * max(1.0, np.abs(ref).max()), err
