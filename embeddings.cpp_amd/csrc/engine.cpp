@@ -352,6 +352,7 @@ bool Device::reserve(int64_t tokens, int64_t seqs)
     const size_t o_qkv = take(rows * 3 * d * 2), o_att = take(rows * d * 2), o_ffn = take(rows * f * 2);
     const size_t o_ids = take(rows * 4), o_cu = take((ns + 1) * 4), o_out = take(ns * d * 4);
     const size_t o_pool = take((size_t)ns * pool_chunks(hp_.n_max_tokens) * d * 4);
+    const size_t o_cnt = take((size_t)(rows / 128 + 1) * 4);   // zero between launches (the last workgroup resets)
     drop_graphs();   // captured graphs hold the old workspace pointers
     if (ws_) { (void)hipFree(ws_); ws_ = nullptr; }
     if (h_ids_) { (void)hipHostFree(h_ids_); h_ids_ = nullptr; }
@@ -367,6 +368,7 @@ bool Device::reserve(int64_t tokens, int64_t seqs)
     qkv_ = (uint16_t *)(ws_ + o_qkv); att_ = (uint16_t *)(ws_ + o_att); ffn_ = (uint16_t *)(ws_ + o_ffn);
     d_ids_ = (int32_t *)(ws_ + o_ids); d_cu_ = (int32_t *)(ws_ + o_cu); d_out_ = (float *)(ws_ + o_out);
     pool_part_ = (float *)(ws_ + o_pool);
+    panel_cnt_ = (uint32_t *)(ws_ + o_cnt);
     HIP_OK(hipHostMalloc((void **)&h_ids_, nt * 4, hipHostMallocDefault));
     HIP_OK(hipHostMalloc((void **)&h_cu_, (ns + 1) * 4, hipHostMallocDefault));
     HIP_OK(hipHostMalloc((void **)&h_out_, ns * d * 4, hipHostMallocDefault));
@@ -510,6 +512,16 @@ int Device::launch_all(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, in
     prev.stats = st_; prev.w = ln_e_w_; prev.b = ln_e_b_;
 
     const double att_flop = 4.0 * (double)d * t * (double)max_len;   // exact when all lengths are equal
+    // the residual GEMM may also run the LayerNorm that follows it (panel LN,
+    // kernels.h ResLN); launch_gemm says whether it did
+    auto panel = [&](const ResLN &in, const float *w, const float *b) {
+        ResLN r = in;
+        if (!panel_ln_ || check) return r;
+        r.cnt = panel_cnt_; r.xh = xh_; r.st_out = st_; r.nw = w; r.nb = b; r.rows = T;
+        static const int pvar = [] { const char *e = std::getenv("BERT_PANEL_VARIANT"); return e ? std::atoi(e) : 0; }();
+        r.pvar = pvar;
+        return r;
+    };
     for (int l = 0; l < hp_.n_layer; ++l) {
         const DevLayer &L = layers_[(size_t)l];
         begin(K_GEMM_QKV, s, ev);
@@ -523,14 +535,16 @@ int Device::launch_all(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, in
         chk("attention", l, att_, (size_t)T * d, 1);
 
         begin(K_GEMM_O, s, ev);
-        launch_gemm(L.o, att_, M, L.b_o, EPI_BIAS_RES, yh_, yh_, s, prev);
+        const int ln1_fused = launch_gemm(L.o, att_, M, L.b_o, EPI_BIAS_RES, yh_, yh_, s, panel(prev, L.ln1_w, L.ln1_b));
         end(K_GEMM_O, s, ev, 2.0 * t * d * d);
         chk("gemm_o", l, yh_, (size_t)T * d, 1);
 
-        begin(K_LAYERNORM, s, ev);
-        launch_layernorm(yh_, T, d, L.ln1_w, L.ln1_b, xh_, st_, s);
+        if (!ln1_fused) {
+            begin(K_LAYERNORM, s, ev);
+            launch_layernorm(yh_, T, d, L.ln1_w, L.ln1_b, xh_, st_, s);
+            end(K_LAYERNORM, s, ev, t * d * 10.0);
+        }
         prev.w = L.ln1_w; prev.b = L.ln1_b;
-        end(K_LAYERNORM, s, ev, t * d * 10.0);
         chk("layernorm1", l, xh_, (size_t)T * d, 1);
 
         begin(K_GEMM_FFN_UP, s, ev);
@@ -539,14 +553,17 @@ int Device::launch_all(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, in
         chk("gemm_up", l, ffn_, (size_t)T * f, 1);
 
         begin(K_GEMM_FFN_DOWN, s, ev);
-        launch_gemm(L.down, ffn_, M, L.b_down, EPI_BIAS_RES, yh_, yh_, s, prev);
+        const int ln2_fused =
+            launch_gemm(L.down, ffn_, M, L.b_down, EPI_BIAS_RES, yh_, yh_, s, panel(prev, L.ln2_w, L.ln2_b));
         end(K_GEMM_FFN_DOWN, s, ev, 2.0 * t * d * f);
         chk("gemm_down", l, yh_, (size_t)T * d, 1);
 
-        begin(K_LAYERNORM, s, ev);
-        launch_layernorm(yh_, T, d, L.ln2_w, L.ln2_b, xh_, st_, s);
+        if (!ln2_fused) {
+            begin(K_LAYERNORM, s, ev);
+            launch_layernorm(yh_, T, d, L.ln2_w, L.ln2_b, xh_, st_, s);
+            end(K_LAYERNORM, s, ev, t * d * 10.0);
+        }
         prev.w = L.ln2_w; prev.b = L.ln2_b;
-        end(K_LAYERNORM, s, ev, t * d * 10.0);
         chk("layernorm2", l, xh_, (size_t)T * d, 1);
     }
     begin(K_POOL_L2, s, ev);
@@ -647,6 +664,75 @@ extern "C" int32_t bertx_test_gemm(int32_t fmt, int32_t N, int32_t K, const void
     HIP_RC(hipMemcpy(out, dout, (size_t)M * N * osz, hipMemcpyDeviceToHost));
     for (char *p : {dq, dd_, dm, dx, db, dr, dout}) if (p) (void)hipFree(p);
     return 0;
+}
+
+// ---------------------------------------------------------------------------
+// residual GEMM + the LayerNorm after it (bert_hip.h): fused panel form or the
+// separate LN kernel, device 0, host buffers
+// ---------------------------------------------------------------------------
+extern "C" int32_t bertx_test_gemm_ln(int32_t fmt, int32_t N, int32_t K, const void *w_rows, const float *bias,
+                                      int32_t M, int32_t rows, const uint16_t *x, const uint16_t *res,
+                                      const float *stats, const float *lnw, const float *lnb, const float *nw,
+                                      const float *nb, uint16_t *out, uint16_t *xh, float *st_out, int32_t panel)
+{
+    using namespace emb;
+    if (!fmt_valid(fmt) || K % 64 || N % 32 || M <= 0 || rows < 0 || rows > M || hip_device_count() == 0) return -1;
+    HostTensor t;
+    t.fmt = fmt; t.ne0 = K; t.ne1 = N;
+    t.bytes.assign((const uint8_t *)w_rows, (const uint8_t *)w_rows + fmt_row_bytes(fmt, K) * (size_t)N);
+    const int fdev = (fmt == FMT_F32 || fmt == FMT_F16) ? FMT_F16 : fmt;
+    Piece q, dd, mm;
+    int n_out = 0, k_out = 0;
+    repack_linear({&t}, fdev, q, dd, mm, n_out, k_out, 1);
+    const int Mp = (int)align_up((size_t)M, GEMM_BM);
+    std::vector<char *> bufs;
+    auto up = [&](const void *h, size_t bytes, size_t alloc) -> char * {
+        char *p = nullptr;
+        if (hipMalloc((void **)&p, std::max<size_t>(alloc, 16)) != hipSuccess) return nullptr;
+        bufs.push_back(p);
+        (void)hipMemset(p, 0, std::max<size_t>(alloc, 16));
+        if (h && bytes) (void)hipMemcpy(p, h, bytes, hipMemcpyHostToDevice);
+        return p;
+    };
+    HIP_RC(hipSetDevice(0));
+    DevWeight W;
+    W.fmt = fdev; W.N = n_out; W.K = k_out; W.layout = 1;
+    W.qs = up(q.bytes.data(), q.bytes.size(), q.bytes.size());
+    W.d = (const uint16_t *)(dd.bytes.empty() ? nullptr : up(dd.bytes.data(), dd.bytes.size(), dd.bytes.size()));
+    W.m = (const uint16_t *)(mm.bytes.empty() ? nullptr : up(mm.bytes.data(), mm.bytes.size(), mm.bytes.size()));
+    char *dx = up(x, (size_t)M * K * 2, (size_t)Mp * K * 2);
+    char *db = up(bias, (size_t)N * 4, (size_t)N * 4);
+    char *dy = up(res, (size_t)M * N * 2, (size_t)Mp * N * 2);   // in place: res -> out
+    char *dst = up(stats, stats ? (size_t)M * 8 : 0, (size_t)Mp * 8);
+    char *dw = up(lnw, (size_t)N * 4, (size_t)N * 4), *dbb = up(lnb, (size_t)N * 4, (size_t)N * 4);
+    char *dnw = up(nw, (size_t)N * 4, (size_t)N * 4), *dnb = up(nb, (size_t)N * 4, (size_t)N * 4);
+    char *dxh = up(nullptr, 0, (size_t)Mp * N * 2);
+    char *dcnt = up(nullptr, 0, (size_t)(Mp / 128 + 1) * 4);
+    int rc = 0;
+    for (char *p : bufs) rc |= p == nullptr;
+    if (!rc) {
+        ResLN r;
+        if (stats) { r.stats = (const float2 *)dst; r.w = (const float *)dw; r.b = (const float *)dbb; }
+        if (panel) {
+            r.cnt = (uint32_t *)dcnt; r.xh = (uint16_t *)dxh; r.st_out = (float2 *)dst;
+            r.nw = (const float *)dnw; r.nb = (const float *)dnb; r.rows = rows;
+        }
+        const int fused = launch_gemm(W, (const uint16_t *)dx, Mp, (const float *)db, EPI_BIAS_RES, dy, dy, nullptr, r);
+        if (panel && !fused) rc = -2;   // this shape has no panel form
+        if (!fused)
+            launch_layernorm((const uint16_t *)dy, rows, N, (const float *)dnw, (const float *)dnb, (uint16_t *)dxh,
+                             (float2 *)dst, nullptr);
+        if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = -1;
+        if (rc == 0) {
+            (void)hipMemcpy(out, dy, (size_t)M * N * 2, hipMemcpyDeviceToHost);
+            (void)hipMemcpy(xh, dxh, (size_t)M * N * 2, hipMemcpyDeviceToHost);
+            (void)hipMemcpy(st_out, dst, (size_t)M * 8, hipMemcpyDeviceToHost);
+        }
+    } else {
+        rc = -1;
+    }
+    for (char *p : bufs) if (p) (void)hipFree(p);
+    return rc;
 }
 
 // ---------------------------------------------------------------------------

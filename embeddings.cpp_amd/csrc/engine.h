@@ -8,6 +8,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -109,6 +110,7 @@ private:
     int32_t *d_ids_ = nullptr, *d_cu_ = nullptr;
     float *d_out_ = nullptr;
     float *pool_part_ = nullptr;
+    uint32_t *panel_cnt_ = nullptr; // per-128-row panel counters of the fused residual LN (ResLN::cnt)
     int32_t *h_ids_ = nullptr, *h_cu_ = nullptr;   // pinned staging
     float *h_out_ = nullptr;
 
@@ -116,6 +118,9 @@ private:
     std::vector<GraphEntry> graphs_;
     std::vector<GraphKey> seen_once_;   // a shape is captured on its second use
     bool use_graphs_ = true;
+    // BERT_PANEL_LN=1 at context creation: residual GEMMs also run the following
+    // LayerNorm (ResLN panel form; measured slower, so off by default)
+    bool panel_ln_ = [] { const char *e = std::getenv("BERT_PANEL_LN"); return e && *e == '1'; }();
 
     // profiling
     bool profiling_ = false;

@@ -787,13 +787,10 @@ void launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, 
     else dispatch_qv<FMT, 128>(W, x, M, bias, epi, res, out, s, rln);
 }
 
-void launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi, const void *res,
-                 void *out, hipStream_t s, const ResLN &rln)
+int launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi, const void *res,
+                void *out, hipStream_t s, const ResLN &rln)
 {
-    if (W.layout == 1) {
-        launch_gemm16(W, X, M, bias, epi, res, out, s, rln);
-        return;
-    }
+    if (W.layout == 1) return launch_gemm16(W, X, M, bias, epi, res, out, s, rln);
     const h16 *x = (const h16 *)X;
     switch (W.fmt) {
     case FMT_Q4_0: launch_fmt<FMT_Q4_0>(W, x, M, bias, epi, res, out, s, rln); break;
@@ -801,6 +798,7 @@ void launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *
     case FMT_Q8_0: launch_fmt<FMT_Q8_0>(W, x, M, bias, epi, res, out, s, rln); break;
     default: launch_fmt<FMT_F16>(W, x, M, bias, epi, res, out, s, rln); break;
     }
+    return 0;
 }
 
 }  // namespace emb

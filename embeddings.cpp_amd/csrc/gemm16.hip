@@ -26,6 +26,7 @@
 #include "device_common.h"
 #include "host_common.h"
 #include "kernels.h"
+#include "rowln.h"
 
 namespace emb {
 
@@ -155,7 +156,25 @@ __device__ __forceinline__ void zswap(float &x, float &y)
     asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
 }
 
-template <int FMT, int EPI, int NW, int BM, int NS>
+// 16-B store that bypasses L1/L2 retention (sc1): the panel hand-off below
+// (MI355X_MICROARCH.md, inter-workgroup visibility: sc1 stores by the
+// producer, agent-scope counter add, agent acquire by the consumer).
+typedef uint32_t zu32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void store16_sc1(void *p, uint4 v)
+{
+    const zu32x4v d = __builtin_bit_cast(zu32x4v, v);
+    // the s_nop covers the "VALU writes the data VGPRs of a >8-byte VMEM store"
+    // hazard, which the compiler's hazard recognizer does not see through asm
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(d) : "memory");
+}
+
+// PLN (residual form only): 0, or NSL = 256-feature slices of a row -- the panel
+// LayerNorm of ResLN (kernels.h) runs in the workgroup that completes its
+// BM-row token panel last.  Opt-in (BERT_PANEL_LN=1): measured slower than the
+// separate LN kernel (profiles/r01_panel_ln_ab.log) -- one workgroup's LN of a
+// 128 x d panel is bound by that CU's load/store bandwidth.  rln.pvar: 0 = tile
+// staged in LDS and stored as whole 128-B lines with sc1, 1 = direct sc1 stores.
+template <int FMT, int EPI, int NW, int BM, int NS, int PLN = 0>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void gemmz_kernel(DevWeight W, const h16 *__restrict__ X,
                                                                const float *__restrict__ bias,
                                                                const void *__restrict__ res, void *__restrict__ out,
@@ -365,9 +384,53 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void gemmz_kernel(DevWeight W, con
                 for (int e = 0; e < 4; ++e)
                     pw[e] = __builtin_bit_cast(uint32_t, h16x2{(h16)v[2 * e], (h16)v[2 * e + 1]});
             }
-            *(uint4 *)((h16 *)out + o) = pk;
+            if constexpr (PLN != 0) {
+                if (rln.pvar == 1) store16_sc1((h16 *)out + o, pk);
+                else {
+                    // stage the tile in LDS (16-B chunk index swizzled by row & 15)
+                    const int rw = tok - m0, ch = (c - n0) >> 3;
+                    *(uint4 *)(smem + (rw << 8) + ((ch ^ (rw & 15)) << 4)) = pk;
+                }
+            } else {
+                *(uint4 *)((h16 *)out + o) = pk;
+            }
         }
     }
+    }
+
+    if constexpr (EPI == EPI_BIAS_RES && PLN != 0) {
+        if (rln.pvar != 1) {
+            // whole 128-B lines from the staged tile: a row's 256 B by 16 lanes
+            __syncthreads();
+            const int ch = tid & 15;
+#pragma unroll
+            for (int i = 0; i < BM / 16; ++i) {
+                const int rw = (tid >> 4) + 16 * i;
+                const uint4 v = *(const uint4 *)(smem + (rw << 8) + ((ch ^ (rw & 15)) << 4));
+                h16 *dst = (h16 *)out + (size_t)(m0 + rw) * N + n0 + 8 * ch;
+                store16_sc1(dst, v);
+            }
+        }
+        // every wave's stores of this tile have landed; then one counter add per
+        // workgroup; the workgroup whose add completes the panel normalises it
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        volatile int *flag = (volatile int *)smem;
+        if (tid == 0) {
+            uint32_t *c = rln.cnt + m0 / BM;
+            const uint32_t old = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int last = old == (uint32_t)(nN - 1);
+            if (last) {
+                __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // ready for the next launch
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            *flag = last;
+        }
+        __syncthreads();
+        if (*flag)
+            ln_rows<4 * PLN, NW>((const h16 *)out, m0, min(m0 + BM, rln.rows), N, wave, lane, rln.nw, rln.nb,
+                             (h16 *)rln.xh, rln.st_out);
     }
 }
 
@@ -387,9 +450,22 @@ void dispatch_z(const DevWeight &W, const h16 *x, int M, const float *bias, int 
 }
 
 template <int FMT>
-void launch_z_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, int32_t epi, const void *res,
-                  void *out, hipStream_t s, const ResLN &rln, int cfg)
+int launch_z_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, int32_t epi, const void *res,
+                 void *out, hipStream_t s, const ResLN &rln, int cfg)
 {
+    // residual form with the panel LayerNorm: 4 waves, 128 x 128 tiles (the
+    // residual form's production shape), every workgroup storing whole tiles
+    if (epi == EPI_BIAS_RES && rln.cnt && (cfg == 0 || cfg == 3) && W.N % 128 == 0 && W.N > 256 &&
+        W.N <= 1024 && M % 128 == 0) {
+        const int nN = W.N / 128, nTiles = (M / 128) * nN;
+        auto go = [&](auto kern) {
+            kern<<<nTiles, 256, 0, s>>>(W, x, bias, res, out, nN, nTiles, rln);
+            return 1;
+        };
+        if (W.N <= 512) return go(gemmz_kernel<FMT, EPI_BIAS_RES, 4, 128, 4, 2>);
+        if (W.N <= 768) return go(gemmz_kernel<FMT, EPI_BIAS_RES, 4, 128, 4, 3>);
+        return go(gemmz_kernel<FMT, EPI_BIAS_RES, 4, 128, 4, 4>);
+    }
     if (cfg == 0) {
         // measured (profiles/r01_gemm16_sweep.log): the residual form (N = d) runs
         // fastest as 128 x 128 tiles two per CU (1536 tiles at bge-base: whole
@@ -401,22 +477,23 @@ void launch_z_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias
     if (cfg == 1) dispatch_z<FMT, 8, 256, 3>(W, x, M, bias, epi, res, out, s, rln);
     else if (cfg == 2) dispatch_z<FMT, 4, 256, 2>(W, x, M, bias, epi, res, out, s, rln);
     else dispatch_z<FMT, 4, 128, 4>(W, x, M, bias, epi, res, out, s, rln);
+    return 0;
 }
 
 }  // namespace
 
 int g_gemm16_cfg = 0;
 
-void launch_gemm16(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi,
-                   const void *res, void *out, hipStream_t s, const ResLN &rln)
+int launch_gemm16(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi,
+                  const void *res, void *out, hipStream_t s, const ResLN &rln)
 {
     const h16 *x = (const h16 *)X;
     const int cfg = g_gemm16_cfg;
     switch (W.fmt) {
-    case FMT_Q4_0: launch_z_fmt<FMT_Q4_0>(W, x, M, bias, epi, res, out, s, rln, cfg); break;
-    case FMT_Q4_1: launch_z_fmt<FMT_Q4_1>(W, x, M, bias, epi, res, out, s, rln, cfg); break;
-    case FMT_Q8_0: launch_z_fmt<FMT_Q8_0>(W, x, M, bias, epi, res, out, s, rln, cfg); break;
-    default: launch_z_fmt<FMT_F16>(W, x, M, bias, epi, res, out, s, rln, cfg); break;
+    case FMT_Q4_0: return launch_z_fmt<FMT_Q4_0>(W, x, M, bias, epi, res, out, s, rln, cfg);
+    case FMT_Q4_1: return launch_z_fmt<FMT_Q4_1>(W, x, M, bias, epi, res, out, s, rln, cfg);
+    case FMT_Q8_0: return launch_z_fmt<FMT_Q8_0>(W, x, M, bias, epi, res, out, s, rln, cfg);
+    default: return launch_z_fmt<FMT_F16>(W, x, M, bias, epi, res, out, s, rln, cfg);
     }
 }
 

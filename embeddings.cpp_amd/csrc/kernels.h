@@ -62,6 +62,18 @@ constexpr int ATT_LDS_MAX = 512;      // sentences up to this length: whole K/V 
 struct ResLN {
     const float2 *stats = nullptr;   // [rows] (mean, 1/sigma); nullptr: residual used as stored
     const float *w = nullptr, *b = nullptr;   // gamma, beta [n_embd]
+    // Panel LayerNorm fused into the residual GEMM (gemm16, EPI_BIAS_RES): the
+    // workgroup that finishes a 128-row token panel last (per-panel counter
+    // `cnt`, zero between launches) normalises the panel's new pre-LN rows with
+    // (nw, nb): xh = f16(LN(out)), st_out = (mean, 1/sigma) for rows < rows.
+    // st_out may alias stats: every reader of the panel's old statistics has
+    // counted in before the last workgroup overwrites them.
+    uint32_t *cnt = nullptr;
+    uint16_t *xh = nullptr;
+    float2 *st_out = nullptr;
+    const float *nw = nullptr, *nb = nullptr;
+    int32_t rows = 0;
+    int32_t pvar = 0;   // panel hand-off variant (gemm16.hip), BERT_PANEL_VARIANT
 };
 __host__ __device__ __forceinline__ float ln_apply(float v, float mean, float scale, float w, float b)
 {
@@ -72,8 +84,11 @@ __host__ __device__ __forceinline__ float ln_apply(float v, float mean, float sc
 // EPI_BIAS_RES: Y = LN(res) + acc + bias (f32 math; res and Y f16, the residual
 // stream) with LN given by `rln` (identity if rln.stats is null); res may alias
 // out (in place, element-wise).
-void launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi,
-                 const void *res, void *out, hipStream_t s, const ResLN &rln = ResLN());
+// Returns 1 when the launch also ran the panel LayerNorm of rln (rln.cnt set,
+// residual form of a gemm16 weight with N % 128 == 0 and N <= 1024), else 0
+// (the caller then runs launch_layernorm itself).
+int launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi,
+                const void *res, void *out, hipStream_t s, const ResLN &rln = ResLN());
 
 // Weight layout 1 (gemm16.hip, v_mfma_f32_16x16x32_f16): per K-step (64 k =
 // blocks 2ks, 2ks+1) and 32-feature group, 64 lane records; lane l = 16g + f
@@ -81,8 +96,8 @@ void launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *
 // elements 8g .. 8g+7): q4 16 B (word u, element i at bit 4(i/2) + 16(i%2)),
 // q8 32 B (8 B per u, (q ^ 0x80) in order e0 e2 e1 e3 per 4-group), f16 64 B;
 // d (and m) f16 [ks][grp][f][u].  N % 32 == 0.
-void launch_gemm16(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi,
-                   const void *res, void *out, hipStream_t s, const ResLN &rln);
+int launch_gemm16(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi,
+                  const void *res, void *out, hipStream_t s, const ResLN &rln);
 // Benches/tests: gemm16 tile config (0 = heuristic, 1 = 8 waves 256x256, 2 = 4 waves 256x128,
 // 3 = 4 waves 128x128).
 extern int g_gemm16_cfg;

@@ -4,6 +4,7 @@
 #include "device_common.h"
 #include "host_common.h"
 #include "kernels.h"
+#include "rowln.h"
 
 #include <cmath>
 
@@ -50,43 +51,6 @@ __device__ __forceinline__ f32x4 table4(const DevTable &t, int row, int c)
     }
 }
 
-// ggml_norm (eps 1e-5, mean then centred variance) * w + b, bert.cpp:977-984.
-// Writes the f16 GEMM input and the row's (mean, 1/sigma); the f32 normalised
-// row itself is not stored -- the next residual epilogue recomputes it from the
-// pre-LN row with ln_apply (kernels.h), the same expression as here.
-__device__ __forceinline__ void ln_row(f32x4 (&v)[MAXV], int d, int lane, const float *w, const float *b, h16 *xh,
-                                       float2 *st)
-{
-    float s = 0.f;
-#pragma unroll
-    for (int k = 0; k < MAXV; ++k) {
-        const int c = 4 * (lane + 64 * k);
-        if (c < d) s += (v[k][0] + v[k][1]) + (v[k][2] + v[k][3]);
-    }
-    const float mean = wave_sum(s) / (float)d;
-    float s2 = 0.f;
-#pragma unroll
-    for (int k = 0; k < MAXV; ++k) {
-        const int c = 4 * (lane + 64 * k);
-        if (c < d) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) { const float u = v[k][e] - mean; s2 += u * u; }
-        }
-    }
-    const float scale = 1.0f / sqrtf(wave_sum(s2) / (float)d + 1e-5f);
-#pragma unroll
-    for (int k = 0; k < MAXV; ++k) {
-        const int c = 4 * (lane + 64 * k);
-        if (c >= d) continue;
-        const f32x4 ww = *(const f32x4 *)(w + c), bb = *(const f32x4 *)(b + c);
-        h16x4 yh;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) yh[e] = (h16)ln_apply(v[k][e], mean, scale, ww[e], bb[e]);
-        *(h16x4 *)(xh + c) = yh;
-    }
-    if (lane == 0) *st = float2{mean, scale};
-}
-
 __global__ __launch_bounds__(256) void embed_ln_kernel(DevTable word, DevTable type, DevTable pos,
                                                        const float *__restrict__ ln_w, const float *__restrict__ ln_b,
                                                        const int32_t *__restrict__ ids, const int32_t *__restrict__ cu,
@@ -114,27 +78,20 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(DevTable word, DevTable t
             *(h16x4 *)(yh + (size_t)t * d + c) = v16;            // pre-LN residual stream
         }
     }
-    ln_row(v, d, lane, ln_w, ln_b, xh + (size_t)t * d, stats + t);
+    ln_row<MAXV>(v, d, lane, ln_w, ln_b, xh + (size_t)t * d, stats + t);
 }
 
+// 32 rows per 256-thread block, 8 lanes per row (rowln.h ln8_*: the same
+// arithmetic as the panel LN fused into the residual GEMM)
 __global__ __launch_bounds__(256) void layernorm_kernel(const h16 *__restrict__ y, int T, int d,
                                                         const float *__restrict__ w, const float *__restrict__ b,
                                                         h16 *__restrict__ xh, float2 *__restrict__ stats)
 {
     const int lane = threadIdx.x & 63;
-    const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (t >= T) return;
-    f32x4 v[MAXV];
-    const h16 *row = y + (size_t)t * d;
-#pragma unroll
-    for (int k = 0; k < MAXV; ++k) {
-        const int c = 4 * (lane + 64 * k);
-        if (c < d) {
-            const h16x4 r = *(const h16x4 *)(row + c);
-            v[k] = f32x4{(float)r[0], (float)r[1], (float)r[2], (float)r[3]};
-        }
-    }
-    ln_row(v, d, lane, w, b, xh + (size_t)t * d, stats + t);
+    const int t = blockIdx.x * 32 + (threadIdx.x >> 3);
+    h16x8 v[16];
+    ln8_load<16>(y, t, t < T, d, lane & 7, v);
+    ln8_row<16>(v, t, t < T, d, lane & 7, w, b, xh, stats);
 }
 
 // pool stage 1: partial column sums of 64-token chunks, weights 1/len
@@ -217,7 +174,7 @@ void launch_embed_ln(const DevTable &word, const DevTable &type, const DevTable 
 void launch_layernorm(const uint16_t *yh, int32_t T, int32_t d, const float *w, const float *b, uint16_t *xh,
                       float2 *stats, hipStream_t s)
 {
-    layernorm_kernel<<<(T + 3) / 4, 256, 0, s>>>((const h16 *)yh, T, d, w, b, (h16 *)xh, stats);
+    layernorm_kernel<<<(T + 31) / 32, 256, 0, s>>>((const h16 *)yh, T, d, w, b, (h16 *)xh, stats);
 }
 
 int32_t pool_chunks(int32_t max_len) { return (max_len + POOL_CHUNK - 1) / POOL_CHUNK; }

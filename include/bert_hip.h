@@ -81,6 +81,20 @@ BERT_API int32_t bertx_test_gemm(int32_t fmt, int32_t N, int32_t K, const void *
                                  int32_t epi, const void *res, void *out, int32_t tile_n);
 
 /*
+ * Residual projection + the LayerNorm that follows it (bert.cpp:1040-1056 and
+ * 1070-1082), host buffers, device 0, gemm16 weights: out f16 [M][N] =
+ * LN(res) + x W^T + bias, with LN(res) from (stats [M] (mean, 1/sigma) as float
+ * pairs, lnw, lnb) or res itself when stats is NULL; then xh f16 [M][N] =
+ * LN(out) with (nw, nb) and st_out [M] its (mean, 1/sigma), for the first `rows`
+ * rows.  panel = 1: the LN runs inside the GEMM (ResLN panel form, -2 if the
+ * shape has none); 0: the separate LN kernel.  Both must give the same bits.
+ */
+BERT_API int32_t bertx_test_gemm_ln(int32_t fmt, int32_t N, int32_t K, const void *w_rows, const float *bias,
+                                    int32_t M, int32_t rows, const uint16_t *x, const uint16_t *res,
+                                    const float *stats, const float *lnw, const float *lnb, const float *nw,
+                                    const float *nb, uint16_t *out, uint16_t *xh, float *st_out, int32_t panel);
+
+/*
  * GEMM micro-benchmark on random operands (device 0): average device time of
  * `iters` launches of the GEMM for fmt / N / K / M / epi.  tile_n: 0 / 128 / 256 =
  * gemm.hip (layout 0) heuristic / tile width; 0x1000 | c = gemm16.hip config c (as

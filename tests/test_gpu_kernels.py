@@ -90,6 +90,56 @@ def test_gemm_matches_numpy(lib, fmt, epi, shape):
         assert np.abs(got - exact).max() <= 5e-3 * np.abs(exact).max()
 
 
+def ln_ref(y, w, b):
+    """ggml_norm (eps 1e-5, mean then centred variance) * w + b (bert.cpp:1048-1056) in f64."""
+    y = y.astype(np.float64)
+    mean = y.mean(axis=1, keepdims=True)
+    sc = 1.0 / np.sqrt(((y - mean) ** 2).mean(axis=1, keepdims=True) + 1e-5)
+    return (y - mean) * sc * w + b, mean[:, 0], sc[:, 0]
+
+
+@pytest.mark.parametrize("fmt", [1, 2, 3, 8])
+@pytest.mark.parametrize("N,K,M,rows", [(768, 768, 512, 500), (384, 1536, 256, 256), (1024, 1024, 384, 257),
+                                        (768, 3072, 256, 129)])
+def test_residual_gemm_panel_layernorm(lib, fmt, N, K, M, rows):
+    """Residual projection + the following LN: the panel form fused into the GEMM
+    (the workgroup completing a 128-row panel normalises it) equals the separate
+    LN kernel bit for bit, and both match numpy (f64) within f16 rounding."""
+    rng = np.random.default_rng(fmt + N + rows)
+    W = rng.standard_normal((N, K)).astype(np.float32) * 0.05
+    wb, deq = weight_rows(fmt, W)
+    bias = rng.standard_normal(N).astype(np.float32) * 0.1
+    X = rng.standard_normal((M, K)).astype(np.float16)
+    res = (rng.standard_normal((M, N)) * 2 + 0.5).astype(np.float16)
+    mean = res.astype(np.float64).mean(axis=1)
+    stats = np.stack([mean, 1.0 / np.sqrt(res.astype(np.float64).var(axis=1) + 1e-5)], axis=1).astype(np.float32)
+    lnw, lnb, nw, nb = (rng.standard_normal(N).astype(np.float32) * s + o
+                        for s, o in ((0.1, 1.0), (0.1, 0.0), (0.2, 1.0), (0.1, 0.0)))
+    outs = []
+    for panel in (1, 0):
+        out = np.zeros((M, N), np.float16)
+        xh = np.zeros((M, N), np.float16)
+        st = stats.copy()
+        rc = lib.bertx_test_gemm_ln(fmt, N, K, wb, bias.ctypes.data, M, rows, X.ctypes.data, res.ctypes.data,
+                                    st.ctypes.data, lnw.ctypes.data, lnb.ctypes.data, nw.ctypes.data,
+                                    nb.ctypes.data, out.ctypes.data, xh.ctypes.data, st.ctypes.data, panel)
+        assert rc == 0, (panel, rc)
+        outs.append((out, xh, st))
+    (o1, x1, s1), (o0, x0, s0) = outs
+    assert np.array_equal(o1.view(np.uint16), o0.view(np.uint16))
+    assert np.array_equal(x1[:rows].view(np.uint16), x0[:rows].view(np.uint16))
+    assert np.array_equal(s1[:rows], s0[:rows])
+    assert np.array_equal(s1[rows:], stats[rows:])              # rows past `rows` untouched
+    # numpy: out = LN(res) + X W^T + bias; xh = LN'(out)
+    r = (res.astype(np.float64) - mean[:, None]) * stats[:, 1:2] * lnw + lnb
+    ref = r + X.astype(np.float64) @ deq.astype(np.float16).astype(np.float64).T + bias
+    assert np.abs(o1 - ref).max() <= 2e-3 * np.abs(ref).max()
+    xref, mref, sref = ln_ref(o1[:rows].astype(np.float64), nw, nb)
+    assert np.abs(x1[:rows] - xref).max() <= 4e-3 * np.abs(xref).max()
+    assert np.allclose(s1[:rows, 0], mref, rtol=1e-4, atol=1e-4)
+    assert np.allclose(s1[:rows, 1], sref, rtol=1e-4)
+
+
 def attention_ref(qkv, cu, n_head, d):
     """f64 softmax(Q K^T / sqrt(dh)) V per (sentence, head) on the f16 inputs (bert.cpp:1018-1036)."""
     dh = d // n_head
