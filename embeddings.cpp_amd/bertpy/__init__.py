@@ -17,7 +17,8 @@ import struct
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-LIB_PATH = os.path.join(ROOT, "build", "libbert.so")
+# BERT_LIB: an A/B build of the same library (scripts/build_variant.sh)
+LIB_PATH = os.environ.get("BERT_LIB") or os.path.join(ROOT, "build", "libbert.so")
 
 FTYPE = {"f32": 0, "f16": 1, "q4_0": 2, "q4_1": 3, "q8_0": 8}
 
