@@ -28,6 +28,7 @@
 #include "kernels.h"
 #include "rowln.h"
 
+#include <cstdio>
 #include <cstdlib>
 #include <utility>
 
@@ -235,6 +236,9 @@ __device__ __forceinline__ void zmma_step(const R &cur, uint32_t xs, uint32_t cx
     zmma_items<NJ, PF>(cur, xs + cx0, xs + cx1, acc, std::make_integer_sequence<int, 2 * NJ>{});
 }
 
+#ifndef EMB_ZBUF
+#define EMB_ZBUF 1
+#endif
 #ifndef EMB_ZPF
 #define EMB_ZPF 4
 #endif
@@ -276,6 +280,25 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void gemmz_kernel(DevWeight W, con
     // LDS-DMA sources: instruction i of this wave fills rows 8*XG*wave + 8i + lane/8;
     // the swizzle ((row>>1)&7) only differs between even and odd i (XG even)
     static_assert(XG % 2 == 0, "XG even");
+#if EMB_ZBUF
+    // as buffer loads: the tile's BM rows are the buffer (out-of-range reads give
+    // 0), one 32-bit offset VGPR per parity of i, the row step in soffset
+    const __amdgpu_buffer_rsrc_t xrs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(X + (size_t)m0 * K), (short)0, BM * K * 2, 0x00020000);
+    uint32_t xvo[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int r = 8 * XG * wave + 8 * i + (lane >> 3);
+        xvo[i] = (uint32_t)(r * K + (((lane & 7) ^ ((r >> 1) & 7)) * 8)) * 2u;
+    }
+#define EMB_ISSUE_XZ(ks_, stage_)                                                                   \
+    {                                                                                               \
+        char *dst_ = smem + (stage_) * XB + ((8 * XG * wave) << 7);                                 \
+        _Pragma("unroll") for (int i = 0; i < XG; ++i)                                              \
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_void_t *)(dst_ + (i << 10)), 16,     \
+                                                     xvo[i & 1], ((i >> 1) * 16 * K + (ks_) * ZK) * 2, 0, 0); \
+    }
+#else
     const h16 *xp[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -289,6 +312,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void gemmz_kernel(DevWeight W, con
         _Pragma("unroll") for (int i = 0; i < XG; ++i)                                              \
             glds<16>(xp[i & 1] + (i >> 1) * xrow8 + (ks_) * ZK, dst_ + (i << 10));                  \
     }
+#endif
     const uint8_t *wq = (const uint8_t *)W.qs + ((size_t)grp * 64 + lane) * QB;
     const uint16_t *wd = W.d + ((size_t)grp * 16 + fr) * 4;
     const uint16_t *wmn = FMT == FMT_Q4_1 ? W.m + ((size_t)grp * 16 + fr) * 4 : nullptr;
@@ -548,12 +572,21 @@ int launch_z_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias,
         return go(gemmz_kernel<FMT, EPI_BIAS_RES, 4, 128, 4, 4>);
     }
     if (cfg == 0) {
-        // measured (profiles/r01_gemm16_sweep.log): the residual form (N = d) runs
-        // fastest as 128 x 128 tiles two per CU (1536 tiles at bge-base: whole
-        // rounds of 512 slots, where 256 x 256 leaves 384 tiles = 1.5 rounds);
-        // the wide forms as one 256 x 256 workgroup per CU once that fills the chip
-        if (epi != EPI_BIAS_RES && W.N % 256 == 0 && (long)(M / 256) * (W.N / 256) >= 256) cfg = 1;
-        else cfg = 3;
+        // measured in the forward at C3 (gpurun_out cfg A/B, r01): 4-wave 256 x 128
+        // tiles two per CU (each wave 32 features x 256 tokens, like the 8-wave
+        // 256 x 256 tile, but the two co-resident workgroups drift apart, so one's
+        // epilogue overlaps the other's MFMAs) beat 256 x 256 for QKV (127 -> 119 us)
+        // and 128 x 128 for FFN-down (158 -> 153 us), tie on FFN-up and O-proj
+        // BERT_GEMM16_CFG="wide,res" overrides the two choices (A/B)
+        static const int2 pick = [] {
+            int2 p{2, 2};
+            if (const char *e = std::getenv("BERT_GEMM16_CFG")) std::sscanf(e, "%d,%d", &p.x, &p.y);
+            return p;
+        }();
+        // below two 256 x 128 tiles per CU (small batches), 128 x 128 tiles
+        const bool fills = M % 256 == 0 && W.N % 128 == 0 && (long)(M / 256) * (W.N / 128) >= 512;
+        cfg = !fills ? 3 : epi != EPI_BIAS_RES ? pick.x : pick.y;
+        if (cfg == 1 && W.N % 256) cfg = 2;
     }
     if (cfg == 1) dispatch_z<FMT, 8, 256, 3>(W, x, M, bias, epi, res, out, s, rln);
     else if (cfg == 2) dispatch_z<FMT, 4, 256, 2>(W, x, M, bias, epi, res, out, s, rln);
