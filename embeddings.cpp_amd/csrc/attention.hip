@@ -603,6 +603,305 @@ __global__ __launch_bounds__(1024) void attention_lds2_kernel(const h16 *__restr
     }
 }
 
+// ---------------------------------------------------------------------------
+// attention_lds3 (production, dh 64): attention_lds2<4>'s arithmetic in a
+// persistent workgroup per CU that walks the items (sentence, head)
+// it = blockIdx.x, + gridDim.x, ..., so the K/V DMA of the next item runs
+// under the current item's MFMAs instead of in front of them (lds2 loads every
+// item in the open: about 16 of its 84 us at C3 were exposed loads).  The K/V
+// image is two regions of 256 keys (A = key blocks 0-3, B = blocks 4-7):
+//   B1 (every wave past the item's region-A blocks): the next item's region-A
+//      K/V pieces are issued;
+//   S  (every wave past its region-B blocks): the item's rows are stored, then
+//      the next item's region-B pieces issued.
+// The vmcnt(0) in front of each barrier retires pieces issued half an item
+// earlier; only a workgroup's first item waits for its loads in the open.  The
+// next item's Q rows are read into the Q registers under the last block's P V
+// (its Q K^T, and any rescale, are done by then).
+// ---------------------------------------------------------------------------
+// the lane id from an asm statement the compiler cannot hoist out of a loop
+__device__ __forceinline__ int lane_id_opaque()
+{
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
+__global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restrict__ qkv,
+                                                              const int32_t *__restrict__ cu, int d, int nh,
+                                                              int n_items, float sl2, h16 *__restrict__ out)
+{
+    constexpr int DH = 64, RB = DH * 2, LMAX = ATT_LDS_MAX, RH = LMAX / 2;
+    static_assert(RH == 256, "a region is 32 pieces: two per wave");
+    __shared__ __attribute__((aligned(16))) char smem[2 * LMAX * RB];
+    char *Kl = smem;
+    const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int hi = lane >> 5, lq = lane & 31;
+    const int ld = 3 * d;
+
+    struct Item { int start, len, h; };
+    auto item = [&](int i) {
+        const int b = i / nh;
+        Item r;
+        r.h = i - b * nh;
+        r.start = cu[b];
+        r.len = cu[b + 1] - r.start;
+        return r;
+    };
+    // region r (rows 256 r .. 256 r + 255) of `it`: piece i = rows 8i .. 8i + 7;
+    // wave w issues pieces 32 r + w and 32 r + w + 16 when they hold rows of the
+    // sentence's 64-row blocks.  K swizzled by (row >> 1) & 7, V by
+    // ((row >> 1) & 1) << 2 (as attention_lds2); rows past the end are finite
+    // copies (masked / P = 0).
+    auto issue = [&](const Item &it, int r) {
+        const int lane = lane_id_opaque();                // recomputed here: hoisted, its
+        const int nrows = (it.len + 63) & ~63;            // derivatives spill around the block loop
+        const h16 *kbase = qkv + (size_t)it.start * ld + d + it.h * DH;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int i = 32 * r + w + 16 * j;
+            if (8 * i < nrows) {
+                const int row = 8 * i + (lane >> 3), pc = lane & 7;
+                const size_t so = (size_t)min(row, it.len - 1) * ld;
+                glds<16>(kbase + so + (pc ^ ((row >> 1) & 7)) * 8, Kl + i * 1024);
+                glds<16>(kbase + d + so + (pc ^ (((row >> 1) & 1) << 2)) * 8, Kl + LMAX * RB + i * 1024);
+            }
+        }
+    };
+    h16x8 qf[DH / 16];
+    auto load_q = [&](const Item &it) {                   // raw rows; scaled at the item's start
+        if (it.len <= 0) return;
+        const int lane = lane_id_opaque(), hi = lane >> 5, lq = lane & 31;
+        const h16 *qrow = qkv + (size_t)(it.start + min(32 * w + lq, it.len - 1)) * ld + it.h * DH;
+#pragma unroll
+        for (int s = 0; s < DH / 16; ++s) qf[s] = *(const h16x8 *)(qrow + 16 * s + 8 * hi);
+    };
+
+    // lane-constant LDS offsets (blocks are 64-row aligned)
+    int koff[DH / 16];
+#pragma unroll
+    for (int st = 0; st < DH / 16; ++st) koff[st] = lq * RB + (((2 * st + hi) ^ ((lq >> 1) & 7)) << 4);
+    const int gi = lane & 15, gq = gi >> 2, gp = gi & 3, gg = lane >> 4;
+    const int vsw = ((gq >> 1) & 1) << 2;
+    int voff[DH / 32];
+#pragma unroll
+    for (int t = 0; t < DH / 32; ++t) {
+        const int ch = 4 * t + 2 * (gg & 1) + (gp >> 1);
+        voff[t] = (4 * (gg >> 1) + gq) * RB + ((ch ^ vsw) << 4) + 8 * (gp & 1);
+    }
+    const h16 one = (h16)1.0f, zero = (h16)0.0f;
+    const h16x8 abias = {hi ? zero : one, zero, zero, zero, zero, zero, zero, zero};
+    h16x8 bbias = {zero, zero, zero, zero, zero, zero, zero, zero};
+
+    f32x16 o[DH / 32];
+    float c = 0.f, l = 0.f;                               // offset (f16-exact), this half's row sum
+    f32x16 s[2];
+    int len = 0;                                          // the current item's
+
+    auto qk = [&](int kb, bool bias) {
+        __builtin_amdgcn_s_setprio(1);
+        int kbo[DH / 16];
+#pragma unroll
+        for (int st = 0; st < DH / 16; ++st) {
+            kbo[st] = koff[st] + kb * RB;
+            asm volatile("" : "+v"(kbo[st]));
+        }
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) {
+            if (bias) {
+                s[kh] = __builtin_amdgcn_mfma_f32_32x32x16_f16(abias, bbias, f32x16{}, 0, 0, 0);
+            } else {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) s[kh][r] = 0.f;
+            }
+#pragma unroll
+            for (int st = 0; st < DH / 16; ++st) {
+                const h16x8 a = *(const h16x8 *)(Kl + kbo[st] + kh * 32 * RB);
+                s[kh] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, qf[st], s[kh], 0, 0, 0);
+            }
+        }
+        __builtin_amdgcn_s_setprio(0);
+        if (kb + 64 > len) {
+#pragma unroll
+            for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int key = kb + 32 * kh + (r & 3) + 8 * (r >> 2) + 4 * hi;
+                    if (key >= len) s[kh][r] = -INFINITY;
+                }
+        }
+    };
+    auto row_max = [&]() {                                // over both halves
+        float mx = s[0][0];
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+            for (int r = (kh ? 0 : 1); r < 16; ++r) mx = fmaxf(mx, s[kh][r]);
+        return halves_max(mx);
+    };
+    auto shift_by = [&](float sh) {                       // scores -= sh
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[kh][r] -= sh;
+    };
+    auto expsum = [&]() {                                 // s <- exp2(s); this half's sum
+        float rs = 0.f;
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float p = __builtin_amdgcn_exp2f(s[kh][r]);
+                s[kh][r] = p;
+                rs += p;
+            }
+        return rs;
+    };
+    auto pv = [&](int kb) {
+        __builtin_amdgcn_s_setprio(1);
+        int vbo[DH / 32];
+#pragma unroll
+        for (int t = 0; t < DH / 32; ++t) {
+            vbo[t] = voff[t] + kb * RB + LMAX * RB;
+            asm volatile("" : "+v"(vbo[t]));
+        }
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) {
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                h16x8 bp;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) bp[j] = (h16)s[kh][8 * s2 + j];
+#pragma unroll
+                for (int t = 0; t < DH / 32; ++t) {
+                    const char *va = smem + vbo[t] + (32 * kh + 16 * s2) * RB;
+                    const h16x4 lo = lds_read_tr16(va);
+                    const h16x4 up = lds_read_tr16(va + 8 * RB);
+                    const h16x8 a = {lo[0], lo[1], lo[2], lo[3], up[0], up[1], up[2], up[3]};
+                    o[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bp, o[t], 0, 0, 0);
+                }
+            }
+        }
+        __builtin_amdgcn_s_setprio(0);
+    };
+    // Q K^T and softmax of block kb > 0 (the first block, peeled off the block loop
+    // as in attention_lds2, sets the offset to its row max)
+    auto scores = [&](int kb) {                           // blocks after the first
+        qk(kb, true);                                     // S - c
+        float rs = expsum();
+        if (__builtin_amdgcn_ballot_w64(rs > (float)(1 << ATT_SUMX))) {
+            // rare: move c to the row max, rescale, redo the block
+            qk(kb, true);
+            const float m = row_max();
+            const float sh = m > 0.f ? (float)(h16)(c + m) - c : 0.f;
+            const float alpha = __builtin_amdgcn_exp2f(-sh);
+            shift_by(sh);
+            c += sh;
+            bbias[0] = hi ? zero : (h16)(-c);
+            l *= alpha;
+#pragma unroll
+            for (int t = 0; t < DH / 32; ++t)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+            rs = expsum();
+        }
+        l += rs;
+    };
+
+    int cur_i = blockIdx.x;
+    if (cur_i >= n_items) return;                         // workgroup-uniform
+    Item cur = item(cur_i);
+    load_q(cur);
+    issue(cur, 0);
+    issue(cur, 1);
+    wait_vmcnt<0>();
+    __syncthreads();
+    const h16 s16 = (h16)sl2;
+    const h16x8 sc = {s16, s16, s16, s16, s16, s16, s16, s16};
+    for (;;) {
+        const int nx_i = cur_i + (int)gridDim.x;
+        const bool more = nx_i < n_items;                 // workgroup-uniform
+        Item nx = {0, 0, 0};
+        if (more) nx = item(nx_i);
+        len = cur.len;
+        const int nrows = (len + 63) & ~63;
+        const bool active = 32 * w < len;                 // wave-uniform
+        // unconditional resets: nothing of the block state stays live across items
+#pragma unroll
+        for (int st = 0; st < DH / 16; ++st) qf[st] *= sc;
+#pragma unroll
+        for (int t = 0; t < DH / 32; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o[t][r] = 0.f;
+        c = 0.f;
+        l = 0.f;
+        bbias[0] = zero;
+        if (active) {                                     // block 0: the offset is its row max (f16-rounded)
+            qk(0, false);
+            c = (float)(h16)row_max();
+            shift_by(c);
+            bbias[0] = hi ? zero : (h16)(-c);
+            l = expsum();
+            pv(0);
+        }
+        bool qnext = false;
+        // blocks 1-7 in one loop (one inlined copy of the block code), B1 at the
+        // region boundary
+#pragma clang loop unroll(disable)
+        for (int kb = 64; kb < LMAX; kb += 64) {
+            if (kb == RH) {
+                wait_vmcnt<0>();                          // this item's region-B pieces
+                __syncthreads();                          // B1: region A is free
+                if (more) issue(nx, 0);
+            }
+            if (active && kb < nrows) {
+                scores(kb);
+                if (more && kb >= RH && kb + 64 >= nrows) {
+                    load_q(nx);
+                    qnext = true;
+                }
+                pv(kb);
+            }
+        }
+        if (more && !qnext) load_q(nx);
+        wait_vmcnt<0>();                                  // the next item's region A and Q
+        __syncthreads();                                  // S: region B is free
+        if (active) {
+            const float inv = 1.0f / halves_sum(l);
+            const int q = 32 * w + lq;
+            if (q < len) {
+                h16 *orow = out + (size_t)(cur.start + q) * d + cur.h * DH;
+#pragma unroll
+                for (int t = 0; t < DH / 32; ++t)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        h16x4 v;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) v[e] = (h16)(o[t][4 * g + e] * inv);
+                        *(h16x4 *)(orow + 32 * t + 8 * g + 4 * hi) = v;
+                    }
+            }
+        }
+        if (!more) break;
+        issue(nx, 1);
+        cur = nx;
+        cur_i = nx_i;
+    }
+}
+
+// CUs of the current device (persistent grids)
+static int att_cus()
+{
+    static const int n = [] {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        return cus;
+    }();
+    return n;
+}
+
 int g_att_variant = 0;   // benches only (bertx_bench_attention)
 
 void launch_attention(const uint16_t *qkv, const int32_t *cu, int32_t n_seqs, int32_t max_len, int32_t n_head,
@@ -613,8 +912,19 @@ void launch_attention(const uint16_t *qkv, const int32_t *cu, int32_t n_seqs, in
     if (max_len <= ATT_LDS_MAX && (dh == 64 || dh == 32)) {
         const dim3 g(n_seqs * n_head), blk(1024);
         if (dh == 64) {
-            // 0: production (attention_lds2, MFMA sections at s_setprio 1); 1: the
-            // previous attention_lds; 2..6: attention_lds2 A/B builds (ABL 0, 1, 2, 3, 5)
+            // 0: production (attention_lds3, persistent, one workgroup per CU); 7:
+            // attention_lds3 on at most 7 workgroups (tests: many items each); 8:
+            // attention_lds2<4> (the previous production, MFMA sections at s_setprio 1);
+            // 1: attention_lds; 2..6: attention_lds2 A/B builds (ABL 0, 1, 2, 3, 5)
+            if (g_att_variant == 0 || g_att_variant == 7) {
+                const int n_items = n_seqs * n_head;
+                const int cap = g_att_variant == 7 ? 7 : att_cus();
+                const int grid = n_items < cap ? n_items : cap;
+                if (grid > 0)
+                    attention_lds3_kernel<<<grid, 1024, 0, s>>>((const h16 *)qkv, cu, d, n_head, n_items, sl2,
+                                                                (h16 *)out);
+                return;
+            }
             decltype(&attention_lds2_kernel<0>) k = attention_lds2_kernel<4>;
             switch (g_att_variant) {
             case 1: k = attention_lds_kernel<64, 0>; break;

@@ -804,8 +804,13 @@ extern "C" int32_t bertx_bench_gemm(int32_t fmt, int32_t N, int32_t K, int32_t M
         const int diag = -3 - ablate;
         // stamped diagnostics: one launch, per-wave phase cycles to stderr
         // tile_n: 256 -> gemmqw 1 x 8, 128 -> gemmqw 2 x 4, 4 -> gemmqv BM 256, 5 -> gemmqv BM 128
+        // tile_n 0x1000 | c: gemm16 config c (1-3) with stamps
+        const int z16 = (tile_n & 0x1000) ? (tile_n & 0xff) : 0;
         const int wm = tile_n == 128 ? 2 : tile_n == 4 ? 4 : tile_n == 5 ? 5 : 1;
-        const int nt = wm >= 4 ? (Mp / 128) * ((N + 127) / 128) * 4 / 8 : (Mp / GEMM_BM) * ((N + 256 / wm - 1) / (256 / wm));
+        const int nt = z16 == 1 ? (Mp / 256) * ((N + 255) / 256)
+                     : z16 == 2 ? (Mp / 256) * ((N + 127) / 128) / 2
+                     : z16 == 3 ? (Mp / 128) * ((N + 127) / 128) / 2
+                     : wm >= 4 ? (Mp / 128) * ((N + 127) / 128) * 4 / 8 : (Mp / GEMM_BM) * ((N + 256 / wm - 1) / (256 / wm));
         // per wave: 4 s_memtime phase stamps (gemmqw: + realtime start/end and the CU id)
         const int SW = wm == 1 ? 8 : 4;
         uint64_t *dst = nullptr;
@@ -817,8 +822,14 @@ extern "C" int32_t bertx_bench_gemm(int32_t fmt, int32_t N, int32_t K, int32_t M
         HIP_RC(hipEventCreate(&e1));
         for (int i = 0; i < 3 + iters; ++i) {
             if (i == 3) HIP_RC(hipEventRecord(e0, nullptr));
-            launch_gemm_q_stamped(W, (const uint16_t *)dx, Mp, (const float *)db, epi, (const void *)dr, dout,
-                                  nullptr, wm, dst, diag);
+            if (z16) {
+                if (W.layout != 1) break;
+                launch_gemm16_stamped(W, (const uint16_t *)dx, Mp, (const float *)db, epi, (const void *)dr, dout,
+                                      nullptr, z16, dst);
+            } else {
+                launch_gemm_q_stamped(W, (const uint16_t *)dx, Mp, (const float *)db, epi, (const void *)dr, dout,
+                                      nullptr, wm, dst, diag);
+            }
         }
         HIP_RC(hipEventRecord(e1, nullptr));
         HIP_RC(hipDeviceSynchronize());

@@ -101,6 +101,8 @@ int launch_gemm16(const DevWeight &W, const uint16_t *X, int32_t M, const float 
 // Benches/tests: gemm16 tile config (0 = heuristic, 1 = 8 waves 256x256, 2 = 4 waves 256x128,
 // 3 = 4 waves 128x128).
 extern int g_gemm16_cfg;
+int launch_gemm16_stamped(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi,
+                          const void *res, void *out, hipStream_t s, int cfg, uint64_t *stamps);
 // Layout the engine repacks linear weights into (BERT_GEMM_LAYOUT overrides).
 extern int g_weight_layout;
 

@@ -94,6 +94,22 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const h16 *__restrict__ 
     ln8_row<16>(v, t, t < T, d, lane & 7, w, b, xh, stats);
 }
 
+// Persistent form (the default): block b normalises the 32-aligned row range
+// [b rpb, min(T, (b + 1) rpb)), its 4 waves 8 rows each per pass with the next
+// pass's loads issued before this pass's arithmetic (rowln.h ln_rows), so the
+// reads and writes of one launch overlap instead of running as one read burst
+// and then one write burst (the one-pass kernel above: every row's wave is
+// resident at once).  The same ln8_row arithmetic, so the same bits.
+template <int NCH>
+__global__ __launch_bounds__(256) void layernorm_rows_kernel(const h16 *__restrict__ y, int T, int d, int rpb,
+                                                             const float *__restrict__ w, const float *__restrict__ b,
+                                                             h16 *__restrict__ xh, float2 *__restrict__ stats)
+{
+    const int r0 = blockIdx.x * rpb;
+    ln_rows<NCH, 4>(y, r0, min(T, r0 + rpb), d, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), threadIdx.x & 63,
+                    w, b, xh, stats);
+}
+
 // pool stage 1: partial column sums of 64-token chunks, weights 1/len
 // (bert.cpp:1087-1089: sum_i X[i][c] * (1/len)).
 constexpr int POOL_CHUNK = 64;
@@ -174,7 +190,33 @@ void launch_embed_ln(const DevTable &word, const DevTable &type, const DevTable 
 void launch_layernorm(const uint16_t *yh, int32_t T, int32_t d, const float *w, const float *b, uint16_t *xh,
                       float2 *stats, hipStream_t s)
 {
-    layernorm_kernel<<<(T + 31) / 32, 256, 0, s>>>((const h16 *)yh, T, d, w, b, (h16 *)xh, stats);
+    if (T <= 0) return;
+    // BERT_LN_BLOCKS (A/B): n > 0 runs the persistent form on n blocks (-1: two per
+    // CU); default the one-pass kernel, measured faster in the forward at C3
+    // (gpurun_out r01h: 21.8 vs 22.7 us at two blocks per CU)
+    static const int nblk = [] {
+        const char *e = std::getenv("BERT_LN_BLOCKS");
+        const int n = e ? std::atoi(e) : 0;
+        if (n >= 0) return n;
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        return 2 * cus;
+    }();
+    if (nblk <= 0) {
+        layernorm_kernel<<<(T + 31) / 32, 256, 0, s>>>((const h16 *)yh, T, d, w, b, (h16 *)xh, stats);
+        return;
+    }
+    const int rpb = ((T + nblk - 1) / nblk + 31) & ~31;
+    const int grid = (T + rpb - 1) / rpb;
+    const h16 *y = (const h16 *)yh;
+    h16 *o = (h16 *)xh;
+    switch (d / 64) {
+    case 6: layernorm_rows_kernel<6><<<grid, 256, 0, s>>>(y, T, d, rpb, w, b, o, stats); break;
+    case 12: layernorm_rows_kernel<12><<<grid, 256, 0, s>>>(y, T, d, rpb, w, b, o, stats); break;
+    default: layernorm_rows_kernel<16><<<grid, 256, 0, s>>>(y, T, d, rpb, w, b, o, stats); break;
+    }
 }
 
 int32_t pool_chunks(int32_t max_len) { return (max_len + POOL_CHUNK - 1) / POOL_CHUNK; }

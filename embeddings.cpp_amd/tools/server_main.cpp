@@ -1,0 +1,193 @@
+// Micro-batching TCP embedding server.
+//
+// The wire protocol is the reference's examples/server.cpp:26-116, unchanged, so
+// examples/sample_client.py talks to it as-is: on connect the server sends the
+// native int32 n_embd; then every recv() of up to 32 KiB is one UTF-8 text and
+// is answered with n_embd raw float32 (zeros when the text tokenizes past the
+// model's n_max_tokens: the reference's refusal leaves its zero-initialised
+// output vector as it was, server.cpp:113-115).
+//
+// The serving model differs.  The reference accepts one client at a time
+// (listen backlog 1) and runs one bert_encode per recv.  Here every connection
+// has its own thread, which tokenizes its text (bert_tokenize, host) and queues
+// it; one batcher thread sends whatever has arrived within --wait-us of the
+// first queued text (at most --max-batch texts) to the GPU as ONE
+// bert_forward_batch.  Per-sentence results do not depend on the batch they ride
+// in (tests/test_gpu_forward.py batch invariance), so every reply equals the
+// single-text result.
+//
+// usage: server -m MODEL [--port P] [-t N] [--max-batch B] [--wait-us U]
+#include "bert.h"
+
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace {
+
+struct Request {
+    std::vector<int32_t> ids;
+    int32_t n_tokens = 0;
+    std::vector<float> emb;
+    bool done = false;
+};
+
+class Batcher {
+public:
+    Batcher(bert_ctx *ctx, int n_threads, int max_batch, int wait_us)
+        : ctx_(ctx), n_threads_(n_threads), max_batch_(max_batch), wait_us_(wait_us)
+    {
+    }
+
+    // queues r and blocks until r->emb holds its embedding
+    void run(Request *r)
+    {
+        std::unique_lock<std::mutex> lk(mu_);
+        queue_.push_back(r);
+        cv_in_.notify_one();
+        cv_out_.wait(lk, [&] { return r->done; });
+    }
+
+    void loop()
+    {
+        std::vector<Request *> batch;
+        std::vector<int32_t *> toks;
+        std::vector<int32_t> lens;
+        std::vector<float *> outs;
+        for (;;) {
+            batch.clear();
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_in_.wait(lk, [&] { return !queue_.empty(); });
+                // the window opens with the first queued text
+                cv_in_.wait_for(lk, std::chrono::microseconds(wait_us_),
+                                [&] { return (int)queue_.size() >= max_batch_; });
+                while (!queue_.empty() && (int)batch.size() < max_batch_) {
+                    batch.push_back(queue_.front());
+                    queue_.pop_front();
+                }
+            }
+            toks.clear();
+            lens.clear();
+            outs.clear();
+            for (Request *r : batch) {
+                toks.push_back(r->ids.data());
+                lens.push_back(r->n_tokens);
+                outs.push_back(r->emb.data());
+            }
+            bert_forward_batch(ctx_, n_threads_, (int32_t)batch.size(), toks.data(), lens.data(), outs.data());
+            {
+                std::lock_guard<std::mutex> g(mu_);
+                for (Request *r : batch) r->done = true;
+            }
+            cv_out_.notify_all();
+        }
+    }
+
+private:
+    bert_ctx *ctx_;
+    int n_threads_, max_batch_, wait_us_;
+    std::mutex mu_;
+    std::condition_variable cv_in_, cv_out_;
+    std::deque<Request *> queue_;
+};
+
+bool send_all(int fd, const void *p, size_t n)
+{
+    const char *c = (const char *)p;
+    while (n) {
+        const ssize_t k = send(fd, c, n, MSG_NOSIGNAL);
+        if (k <= 0) return false;
+        c += k;
+        n -= (size_t)k;
+    }
+    return true;
+}
+
+void serve(int fd, bert_ctx *ctx, Batcher *b)
+{
+    const int32_t n_embd = bert_n_embd(ctx), n_max = bert_n_max_tokens(ctx);
+    int one = 1;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+    if (send_all(fd, &n_embd, sizeof(n_embd))) {
+        std::vector<char> buf((size_t)1 << 15);      // server.cpp:27
+        for (;;) {
+            const ssize_t k = recv(fd, buf.data(), buf.size(), 0);
+            if (k <= 0) break;
+            const std::string text(buf.data(), (size_t)k);
+            Request r;
+            r.ids.resize((size_t)n_max);
+            bert_tokenize(ctx, text.c_str(), r.ids.data(), &r.n_tokens, n_max);
+            r.emb.assign((size_t)n_embd, 0.0f);
+            if (r.n_tokens > 0 && r.n_tokens <= n_max) b->run(&r);
+            if (!send_all(fd, r.emb.data(), r.emb.size() * sizeof(float))) break;
+        }
+    }
+    close(fd);
+}
+
+}  // namespace
+
+int main(int argc, char **argv)
+{
+    int max_batch = 64, wait_us = 2000;
+    std::vector<char *> rest;
+    for (int i = 0; i < argc; ++i) {
+        if (i > 0 && i + 1 < argc && !std::strcmp(argv[i], "--max-batch")) { max_batch = std::atoi(argv[++i]); continue; }
+        if (i > 0 && i + 1 < argc && !std::strcmp(argv[i], "--wait-us")) { wait_us = std::atoi(argv[++i]); continue; }
+        rest.push_back(argv[i]);
+    }
+    bert_params params;
+    if (!bert_params_parse((int)rest.size(), rest.data(), params)) return 1;
+    if (max_batch < 1) max_batch = 1;
+    if (wait_us < 0) wait_us = 0;
+
+    bert_ctx *ctx = bert_load_from_file(params.model);
+    if (!ctx) {
+        std::fprintf(stderr, "%s: failed to load model from '%s'\n", __func__, params.model);
+        return 1;
+    }
+    const int srv = socket(AF_INET, SOCK_STREAM, 0);
+    if (srv < 0) {
+        std::perror("socket");
+        return 1;
+    }
+    int one = 1;
+    setsockopt(srv, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+    sockaddr_in addr{};
+    addr.sin_family = AF_INET;
+    addr.sin_addr.s_addr = INADDR_ANY;
+    addr.sin_port = htons((uint16_t)params.port);
+    if (bind(srv, (sockaddr *)&addr, sizeof(addr)) < 0 || listen(srv, 128) < 0) {
+        std::perror("bind/listen");
+        return 1;
+    }
+    std::printf("Server running on port %d: up to %d texts per GPU batch, %d us window\n", params.port, max_batch,
+                wait_us);
+    std::fflush(stdout);
+    Batcher batcher(ctx, params.n_threads, max_batch, wait_us);
+    std::thread(&Batcher::loop, &batcher).detach();
+    for (;;) {
+        const int fd = accept(srv, nullptr, nullptr);
+        if (fd < 0) {
+            if (errno == EINTR || errno == ECONNABORTED) continue;
+            std::perror("accept");
+            return 1;
+        }
+        std::thread(serve, fd, ctx, &batcher).detach();
+    }
+}

@@ -56,7 +56,9 @@ def run_gemm(lib, fmt, W, bias, X, epi, res=None, tile_n=0):
                                    # gemm16 (layout 1) configs: 0x1000 | 1 (8 waves 256x256),
                                    # 2 (4 waves 256x128), 3 (4 waves 128x128)
                                    (768, 768, 512, 0x1001), (2304, 768, 768, 0x1002), (448, 192, 700, 0x1003),
-                                   (256, 3072, 256, 0x1001)])
+                                   (256, 3072, 256, 0x1001),
+                                   # 0x1004: the ping-pong kernel (8 waves, 256 x 256, halves alternating)
+                                   (768, 768, 512, 0x1004), (512, 3072, 768, 0x1004), (2304, 192, 256, 0x1004)])
 def test_gemm_matches_numpy(lib, fmt, epi, shape):
     N, K, M, tile_n = shape
     if tile_n == 256 and epi == 2:   # gemm.hip's 256-wide tile has no residual form
@@ -88,6 +90,31 @@ def test_gemm_matches_numpy(lib, fmt, epi, shape):
     exact = xh.astype(np.float64) @ deq.astype(np.float64).T + bias
     if epi == 0:
         assert np.abs(got - exact).max() <= 5e-3 * np.abs(exact).max()
+
+
+@pytest.mark.parametrize("N,K,M,epi", [(2304, 768, 8192, 0), (3072, 768, 8192, 1), (768, 3072, 32768, 2)])
+def test_gemm_column_split_bitwise(lib, N, K, M, epi):
+    """gemm16's column split (gemmz_split_kernel, chosen by the heuristic when a grid of
+    256 x 128 tiles is not whole rounds of two per CU: its last columns run as 128 x 128
+    tiles in the same launch) gives the bits of the unsplit 256 x 128 grid, and numpy
+    within f16 rounding."""
+    rng = np.random.default_rng(N + K + epi)
+    W = rng.standard_normal((N, K)).astype(np.float32) * 0.05
+    bias = rng.standard_normal(N).astype(np.float32) * 0.1
+    X = rng.standard_normal((M, K)).astype(np.float32)
+    res = rng.standard_normal((M, N)).astype(np.float16) if epi == 2 else None
+    split, deq, xh = run_gemm(lib, 2, W, bias, X, epi, res, 0x1005)     # split grid
+    whole, _, _ = run_gemm(lib, 2, W, bias, X, epi, res, 0x1002)        # 256 x 128 everywhere
+    assert np.array_equal(split, whole)
+    acc = xh.astype(np.float64) @ deq.astype(np.float16).astype(np.float64).T + bias
+    if epi == 1:
+        x16 = acc.astype(np.float16).astype(np.float64)
+        ref = 0.5 * x16 * (1 + np.tanh(0.7978845608028654 * x16 * (1 + 0.044715 * x16 * x16)))
+    elif epi == 2:
+        ref = res.astype(np.float64) + acc
+    else:
+        ref = acc
+    assert np.abs(split - ref).max() <= 3e-3 * np.abs(ref).max()
 
 
 def ln_ref(y, w, b):
@@ -155,7 +182,8 @@ def attention_ref(qkv, cu, n_head, d):
     return out
 
 
-@pytest.mark.parametrize("variant,dh", [(0, 64), (1, 64), (2, 64), (6, 64), (-1, 64), (0, 32), (-1, 32)])
+@pytest.mark.parametrize("variant,dh", [(0, 64), (7, 64), (8, 64), (1, 64), (2, 64), (6, 64), (-1, 64), (0, 32),
+                                        (-1, 32)])
 def test_attention_matches_numpy(lib, variant, dh):
     """Ragged sentences (1 .. 512 tokens, block edges), one with sharp scores whose row
     maximum moves late (exercises the deferred-max rescale of variant 2)."""
