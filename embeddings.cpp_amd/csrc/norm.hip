@@ -81,6 +81,44 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(DevTable word, DevTable t
     ln_row<MAXV>(v, d, lane, ln_w, ln_b, xh + (size_t)t * d, stats + t);
 }
 
+// 32 rows per 256-thread block, 8 lanes per row (as layernorm_kernel): lane sub
+// of a row group gathers the 16-B chunks at features 8 sub + 64 k of the three
+// tables, so a wave has 8 rows' gathers in flight (the one-wave-per-row kernel
+// above has one), then ln8_row normalises the f16-rounded residual row.
+__global__ __launch_bounds__(256) void embed_ln8_kernel(DevTable word, DevTable type, DevTable pos,
+                                                        const float *__restrict__ ln_w, const float *__restrict__ ln_b,
+                                                        const int32_t *__restrict__ ids, const int32_t *__restrict__ cu,
+                                                        int d, h16 *__restrict__ yh, h16 *__restrict__ xh,
+                                                        float2 *__restrict__ stats)
+{
+    const int b = blockIdx.y, sub = threadIdx.x & 7;
+    const int i = blockIdx.x * 32 + (threadIdx.x >> 3);
+    const int start = cu[b], len = cu[b + 1] - start;
+    const bool valid = i < len;
+    const int t = start + (valid ? i : 0);
+    h16x8 v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = h16x8{};
+    if (valid) {
+        const int id = ids[t];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int c = 8 * sub + 64 * k;
+            if (64 * k >= d) continue;
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+                // pos + (type[0] + word[id])  (bert.cpp:968-973 operand order)
+                const f32x4 w = table4(word, id, c + 4 * hf), ty = table4(type, 0, c + 4 * hf),
+                            p = table4(pos, i, c + 4 * hf);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[k][4 * hf + e] = (h16)(p[e] + (ty[e] + w[e]));
+            }
+            *(h16x8 *)(yh + (size_t)t * d + c) = v[k];       // pre-LN residual stream
+        }
+    }
+    ln8_row<16>(v, t, valid, d, sub, ln_w, ln_b, xh, stats);
+}
+
 // 32 rows per 256-thread block, 8 lanes per row (rowln.h ln8_*: the same
 // arithmetic as the panel LN fused into the residual GEMM)
 __global__ __launch_bounds__(256) void layernorm_kernel(const h16 *__restrict__ y, int T, int d,
@@ -119,22 +157,43 @@ __global__ __launch_bounds__(256) void pool_partial_kernel(const h16 *__restrict
                                                            const int32_t *__restrict__ cu, int d, int n_chunks,
                                                            float *__restrict__ part)
 {
-    const int b = blockIdx.y, ch = blockIdx.x;
+    // thread t owns 8 columns (16-B loads) of every TT-th token of the chunk:
+    // column group t % G (G = d / 8 <= 128), token lane t / G; the token lanes
+    // are summed through LDS in a fixed order
+    __shared__ f32x4 red[256][2];
+    const int b = blockIdx.y, ch = blockIdx.x, tid = threadIdx.x;
     const int start = cu[b], len = cu[b + 1] - start;
-    const int i0 = ch * POOL_CHUNK;
-    float *dst = part + ((size_t)b * n_chunks + ch) * d;
+    const int i0 = ch * POOL_CHUNK, i1 = min(len, i0 + POOL_CHUNK);
+    const int G = d / 8, TT = 256 / G, cg = tid % G, tl = tid / G;
     const float wt = 1.0f / (float)len;
-    for (int c = 4 * threadIdx.x; c < d; c += 4 * 256) {
-        f32x4 a = {0.f, 0.f, 0.f, 0.f};
-        const f32x4 ww = *(const f32x4 *)(lw + c), bb = *(const f32x4 *)(lb + c);
-        const int i1 = min(len, i0 + POOL_CHUNK);
-        for (int i = i0; i < i1; ++i) {
-            const h16x4 y = *(const h16x4 *)(y32 + (size_t)(start + i) * d + c);
+    f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
+    if (tl < TT) {
+        const int c = 8 * cg;
+        const f32x4 w0 = *(const f32x4 *)(lw + c), w1 = *(const f32x4 *)(lw + c + 4);
+        const f32x4 b0 = *(const f32x4 *)(lb + c), b1 = *(const f32x4 *)(lb + c + 4);
+#pragma unroll 4
+        for (int i = i0 + tl; i < i1; i += TT) {
+            const h16x8 y = *(const h16x8 *)(y32 + (size_t)(start + i) * d + c);
             const float2 st = stats[start + i];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) a[e] += ln_apply((float)y[e], st.x, st.y, ww[e], bb[e]) * wt;
+            for (int e = 0; e < 4; ++e) {
+                a0[e] += ln_apply((float)y[e], st.x, st.y, w0[e], b0[e]) * wt;
+                a1[e] += ln_apply((float)y[4 + e], st.x, st.y, w1[e], b1[e]) * wt;
+            }
         }
-        *(f32x4 *)(dst + c) = a;
+    }
+    red[tid][0] = a0;
+    red[tid][1] = a1;
+    __syncthreads();
+    if (tid < G) {
+        f32x4 s0 = red[tid][0], s1 = red[tid][1];
+        for (int k = 1; k < TT; ++k) {
+            s0 += red[tid + k * G][0];
+            s1 += red[tid + k * G][1];
+        }
+        float *dst = part + ((size_t)b * n_chunks + ch) * d + 8 * tid;
+        *(f32x4 *)dst = s0;
+        *(f32x4 *)(dst + 4) = s1;
     }
 }
 
@@ -183,8 +242,17 @@ void launch_embed_ln(const DevTable &word, const DevTable &type, const DevTable 
                      const float *ln_b, const int32_t *ids, const int32_t *cu, int32_t n_seqs, int32_t max_len,
                      int32_t d, uint16_t *yh, uint16_t *xh, float2 *stats, hipStream_t s)
 {
-    dim3 grid((max_len + 3) / 4, n_seqs);
-    embed_ln_kernel<<<grid, 256, 0, s>>>(word, type, pos, ln_w, ln_b, ids, cu, d, (h16 *)yh, (h16 *)xh, stats);
+    // the one-wave-per-row kernel by default; BERT_EMBED_LN8=1 (A/B) runs the
+    // 8-lanes-per-row form, measured no faster (53.0 vs 51.9 us at C3, gpurun_out r01j:
+    // the table gathers, not the row sums, bound it)
+    static const bool rowwave = [] { const char *e = std::getenv("BERT_EMBED_LN8"); return !(e && *e == '1'); }();
+    if (rowwave) {
+        dim3 grid((max_len + 3) / 4, n_seqs);
+        embed_ln_kernel<<<grid, 256, 0, s>>>(word, type, pos, ln_w, ln_b, ids, cu, d, (h16 *)yh, (h16 *)xh, stats);
+        return;
+    }
+    dim3 grid((max_len + 31) / 32, n_seqs);
+    embed_ln8_kernel<<<grid, 256, 0, s>>>(word, type, pos, ln_w, ln_b, ids, cu, d, (h16 *)yh, (h16 *)xh, stats);
 }
 
 void launch_layernorm(const uint16_t *yh, int32_t T, int32_t d, const float *w, const float *b, uint16_t *xh,
