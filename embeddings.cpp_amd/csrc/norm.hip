@@ -132,12 +132,11 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const h16 *__restrict__ 
     ln8_row<16>(v, t, t < T, d, lane & 7, w, b, xh, stats);
 }
 
-// Persistent form (the default): block b normalises the 32-aligned row range
-// [b rpb, min(T, (b + 1) rpb)), its 4 waves 8 rows each per pass with the next
-// pass's loads issued before this pass's arithmetic (rowln.h ln_rows), so the
-// reads and writes of one launch overlap instead of running as one read burst
-// and then one write burst (the one-pass kernel above: every row's wave is
-// resident at once).  The same ln8_row arithmetic, so the same bits.
+// Persistent form (A/B via BERT_LN_BLOCKS, measured slower): block b normalises
+// the 32-aligned row range [b rpb, min(T, (b + 1) rpb)), its 4 waves 8 rows each
+// per pass with the next pass's loads issued before this pass's arithmetic
+// (rowln.h ln_rows), so the reads and writes of one launch overlap.  The same
+// ln8_row arithmetic as the one-pass kernel above, so the same bits.
 template <int NCH>
 __global__ __launch_bounds__(256) void layernorm_rows_kernel(const h16 *__restrict__ y, int T, int d, int rpb,
                                                              const float *__restrict__ w, const float *__restrict__ b,
