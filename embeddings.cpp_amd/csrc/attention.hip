@@ -811,11 +811,13 @@ __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restr
     int cur_i = blockIdx.x;
     if (cur_i >= n_items) return;                         // workgroup-uniform
     Item cur = item(cur_i);
+    // the first item: Q and region A in the open; region B under region A's
+    // blocks (retired by B1's wait, as in every later item)
     load_q(cur);
     issue(cur, 0);
-    issue(cur, 1);
     wait_vmcnt<0>();
     __syncthreads();
+    issue(cur, 1);
     const h16 s16 = (h16)sl2;
     const h16x8 sc = {s16, s16, s16, s16, s16, s16, s16, s16};
     for (;;) {
