@@ -713,7 +713,10 @@ int z_slots()
 // Measured in the forward at C3 (gpurun_out r01g): QKV 114 -> 119 us, FFN-down
 // 149.4 -> 148.3, O-proj 59.3 -> 58.3, 8,927 -> 8,760 sentences/s -- the lone
 // workgroups of the part-filled round run nearly twice as fast as paired ones,
-// so that round costs far less than a full one.  Off by default:
+// so that round costs far less than a full one.  For the residual forms alone
+// (BERT_GEMM16_SPLIT=r) the evented kernel times improve (O-proj 60.2 -> 57.4,
+// FFN-down 149.7 -> 148.5 us) but the graph-replayed forward does not (9,010 ->
+// 8,888 sentences/s, three runs each, gpurun_out r01m).  Off by default:
 // BERT_GEMM16_SPLIT=1 turns it on (A/B); tile config 5 forces it (tests).
 int z_split_cols(int M, int N)
 {
@@ -1003,8 +1006,12 @@ int launch_z_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias,
         if (W.N <= 768) return go(gemmz_kernel<FMT, EPI_BIAS_RES, 4, 128, 4, 3>);
         return go(gemmz_kernel<FMT, EPI_BIAS_RES, 4, 128, 4, 4>);
     }
-    static const bool split_env = [] { const char *e = std::getenv("BERT_GEMM16_SPLIT"); return e && *e == '1'; }();
-    const bool split = cfg == 5 || (cfg == 0 && split_env);
+    // BERT_GEMM16_SPLIT: 1 every form, r the residual forms only, else none (A/B)
+    static const int split_env = [] {
+        const char *e = std::getenv("BERT_GEMM16_SPLIT");
+        return !e ? 0 : *e == '1' ? 1 : *e == 'r' ? 2 : 0;
+    }();
+    const bool split = cfg == 5 || (cfg == 0 && (split_env == 1 || (split_env == 2 && epi == EPI_BIAS_RES)));
     if (cfg == 5) cfg = 2;
     if (cfg == 0) {
         // measured in the forward at C3 (gpurun_out cfg A/B, r01): 4-wave 256 x 128
