@@ -41,6 +41,7 @@ def parse():
     p.add_argument("--cpu-baseline-sentences", type=int, default=24)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-profile", action="store_true", help="disable live per-kernel event timing")
+    p.add_argument("--no-probes", action="store_true", help="skip the north-star probes (C2 f16, B=1 L=32 q4_0)")
     return p.parse_args()
 
 
@@ -83,6 +84,135 @@ def timed_steps(step, steps, sync, dist=None, reduce_device="cpu"):
     return elapsed
 
 
+class DeviceForward:
+    """One model's device-resident forward (bertx_forward_device) on HBM-resident
+    ids, captured into a HIP graph by the library on its second use."""
+
+    def __init__(self, lib, bertpy, torch, path, ids_list, dev, stream):
+        import numpy as np
+        self.lib, self.torch, self.dev = lib, torch, dev
+        self.model = bertpy.BertModel(path, lib=lib)
+        ctx = self.model.ctx
+        B = len(ids_list)
+        lens = [len(x) for x in ids_list]
+        self.B, self.T, self.L = B, sum(lens), max(lens)
+        self.ids = torch.from_numpy(np.concatenate(ids_list).astype(np.int32)).to(dev)
+        self.cu = torch.from_numpy(np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)).to(dev)
+        self.out = torch.empty((B, self.model.n_embd), dtype=torch.float32, device=dev)
+        assert lib.bertx_reserve(ctx, 0, self.T, B) == 0
+        self.sp = ctypes.c_void_p(stream.cuda_stream)
+        self.args = (ctx, 0, ctypes.c_void_p(self.ids.data_ptr()), ctypes.c_void_p(self.cu.data_ptr()), B, self.L,
+                     self.T, ctypes.c_void_p(self.out.data_ptr()), self.sp)
+
+    def step(self):
+        rc = self.lib.bertx_forward_device(*self.args)
+        if rc != 0:
+            raise RuntimeError(f"bertx_forward_device failed: {rc}")
+
+    def sync(self):
+        self.torch.cuda.synchronize(self.dev)
+
+    def check(self):
+        import numpy as np
+        e = self.out.float().cpu().numpy()
+        assert np.all(np.isfinite(e)) and np.allclose(np.linalg.norm(e, axis=1), 1.0, atol=1e-3), "bad embeddings"
+        return e
+
+    def kernel_pass(self, steps):
+        """K eager forwards with a HIP event pair around every kernel on the
+        launch stream; returns the per-class stats."""
+        ctx = self.model.ctx
+        self.lib.bertx_set_profiling(ctx, 1)
+        self.lib.bertx_reset_stats(ctx)
+        t = timed_steps(self.step, steps, self.sync)
+        self.lib.bertx_set_profiling(ctx, 0)
+        return t, self.model.kernel_stats()
+
+
+def ensure_model(bertpy, model_dir, arch, ftype, seed):
+    os.makedirs(model_dir, exist_ok=True)
+    path = os.path.join(model_dir, f"{arch}-{ftype}-seed{seed}.bin")
+    if not os.path.exists(path):
+        bertpy.synthetic_model(path + ".part", arch, ftype, seed=seed)
+        os.replace(path + ".part", path)
+    return path
+
+
+def dominant(stats):
+    """(class name, avg launch seconds, work per launch, work is FLOP) of the class with the most time."""
+    live = [s for s in stats if s["launches"]]
+    if not live:
+        return None
+    dom = max(live, key=lambda s: s["ms"])
+    return dom["name"], dom["ms"] / dom["launches"] * 1e-3, dom["work"] / dom["launches"], dom["work_is_flops"]
+
+
+def probes(lib, bertpy, torch, a, dev, stream, q4_path):
+    """BASELINE.json north_star: 'rocprof reports achieved HBM GB/s on the q4_0 path and
+    MFMA utilisation on the f16 path against gfx950 peak'.  Two probes, each timed
+    like the headline (graph replay between syncs, then an evented pass):
+      f16_mfma: C2 = all-MiniLM-L6-v2 f16, L 128, B 32 -- sentences/s and the
+        dominant kernel's achieved TFLOP/s against the 2.5 PF dense f16 peak;
+      q4_0_hbm: bge-base q4_0, B 1, L 32 (SURVEY §8d's bandwidth-bound probe, AI ~40)
+        -- forward latency and algorithmic bytes (weights at stored width + rows +
+        ids + output) / latency against 8 TB/s.  PMC traffic of the same run:
+        profiles/r02_probe_q4_0_b1_pmc.json."""
+    out = {}
+    steps = max(a.steps, 20)
+    # C2
+    hp = bertpy.ARCHS["all-MiniLM-L6-v2"]
+    p2 = ensure_model(bertpy, a.model_dir, "all-MiniLM-L6-v2", "f16", a.seed)
+    f = DeviceForward(lib, bertpy, torch, p2, bertpy.synthetic_ids(32, 128, hp["n_vocab"], seed=7), dev, stream)
+    for _ in range(3):
+        f.step()
+    f.sync()
+    f.check()
+    el = timed_steps(f.step, steps, f.sync)
+    _, st = f.kernel_pass(steps)
+    name, avg_s, work, is_flops = dominant(st)
+    ach = work / avg_s / 1e12
+    out["f16_mfma"] = {"workload": "C2 all-MiniLM-L6-v2 f16, L 128, B 32 (bertx_forward_device)",
+                       "sentences_per_s": round(32 * steps / el, 1), "ms_per_batch": round(el / steps * 1e3, 4),
+                       "dominant_kernel": name, "avg_launch_us": round(avg_s * 1e6, 2),
+                       "achieved_tflops": round(ach, 1), "peak_tflops": MFMA_F16_PEAK_TFLOPS,
+                       "mfma_frac": round(ach / MFMA_F16_PEAK_TFLOPS, 4),
+                       "step_tflops": round(32 * flop_per_sentence(hp, 128) * steps / el / 1e12, 1)}
+    del f
+    # bandwidth probe: bge-base q4_0, one sentence of 32 tokens
+    hp = bertpy.ARCHS["bge-base-en-v1.5"]
+    f = DeviceForward(lib, bertpy, torch, q4_path, bertpy.synthetic_ids(1, 32, hp["n_vocab"], seed=7), dev, stream)
+    for _ in range(3):
+        f.step()
+    f.sync()
+    f.check()
+    steps_b = max(200, steps)
+    el = timed_steps(f.step, steps_b, f.sync)
+    lat = el / steps_b
+    by = algorithmic_bytes(hp, "q4_0", 1, 32)
+    _, st = f.kernel_pass(steps_b)
+    launches = sum(s["launches"] for s in st) / steps_b
+    kern_s = sum(s["ms"] for s in st) * 1e-3 / steps_b
+    out["q4_0_hbm"] = {"workload": "bge-base-en-v1.5 q4_0, B 1, L 32 (bertx_forward_device)",
+                       "latency_us": round(lat * 1e6, 1), "algorithmic_bytes": int(by),
+                       "achieved_gbps": round(by / lat / 1e9, 1), "peak_gbps": HBM_PEAK_GBPS,
+                       "hbm_frac": round(by / lat / 1e9 / HBM_PEAK_GBPS, 4),
+                       "kernels_per_forward": launches, "sum_kernel_us": round(kern_s * 1e6, 1)}
+    pmc = os.path.join(ROOT, "profiles", "r02_probe_q4_0_b1_pmc.json")
+    if os.path.exists(pmc):
+        try:
+            with open(pmc) as fh:
+                out["q4_0_hbm"]["pmc"] = json.load(fh)
+        except Exception:
+            pass
+    del f
+    return out
+
+
+def flop_per_sentence(hp, L):
+    d, f, nl = hp["n_embd"], hp["n_intermediate"], hp["n_layer"]
+    return nl * (2 * L * (4 * d * d + 2 * d * f) + 4 * L * L * d)
+
+
 def main():
     a = parse()
     rank, world, local = dist_env()
@@ -102,56 +232,41 @@ def main():
         torch.cuda.set_device(local)
 
     hp = bertpy.ARCHS[a.arch]
-    os.makedirs(a.model_dir, exist_ok=True)
     path = os.path.join(a.model_dir, f"{a.arch}-{a.ftype}-seed{a.seed}.bin")
-    if rank == 0 and not os.path.exists(path):
-        bertpy.synthetic_model(path + ".part", a.arch, a.ftype, seed=a.seed)
-        os.replace(path + ".part", path)
+    if rank == 0:
+        path = ensure_model(bertpy, a.model_dir, a.arch, a.ftype, a.seed)
     if dist is not None:
         dist.barrier()
 
     lib = bertpy.load_lib()
-    model = bertpy.BertModel(path, lib=lib)
-    ctx = model.ctx
-    d = model.n_embd
-    B, L = a.batch, a.seq
-    ids_list = bertpy.synthetic_ids(B, L, hp["n_vocab"], seed=7 + rank)
     dev = torch.device("cuda", local)
-    ids = torch.from_numpy(np.concatenate(ids_list).astype(np.int32)).to(dev)
-    cu = torch.arange(0, (B + 1) * L, L, dtype=torch.int32).to(dev)
-    out = torch.empty((B, d), dtype=torch.float32, device=dev)
-    T = B * L
-    assert lib.bertx_reserve(ctx, 0, T, B) == 0
     # a non-default stream: the library captures the forward into a HIP graph
     # (capture is impossible on the legacy null stream)
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
-    sp = ctypes.c_void_p(stream.cuda_stream)
-
-    def step():
-        rc = lib.bertx_forward_device(ctx, 0, ctypes.c_void_p(ids.data_ptr()), ctypes.c_void_p(cu.data_ptr()),
-                                      B, L, T, ctypes.c_void_p(out.data_ptr()), sp)
-        if rc != 0:
-            raise RuntimeError(f"bertx_forward_device failed: {rc}")
+    B, L = a.batch, a.seq
+    ids_list = bertpy.synthetic_ids(B, L, hp["n_vocab"], seed=7 + rank)
+    fwd = DeviceForward(lib, bertpy, torch, path, ids_list, dev, stream)
+    model, step = fwd.model, fwd.step
+    d = model.n_embd
 
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize(dev)
-    e = out.float().cpu().numpy()
-    assert np.all(np.isfinite(e)) and np.allclose(np.linalg.norm(e, axis=1), 1.0, atol=1e-3), "bad embeddings"
+    e = fwd.check()
 
     red_dev = dev if (dist is not None and dist.get_backend() == "nccl") else "cpu"
     # timed region (the metric): graph replay of the forward, no per-kernel events
-    lib.bertx_set_profiling(ctx, 0)
+    lib.bertx_set_profiling(model.ctx, 0)
     elapsed = timed_steps(step, a.steps, lambda: torch.cuda.synchronize(dev), dist, red_dev)
     # roofline pass: the same K steps again, launched eagerly with a HIP event
     # pair around every kernel on the launch stream (per-kernel averages)
     stats = []
     if not a.no_profile:
-        lib.bertx_set_profiling(ctx, 1)
-        lib.bertx_reset_stats(ctx)
+        lib.bertx_set_profiling(model.ctx, 1)
+        lib.bertx_reset_stats(model.ctx)
         prof_elapsed = timed_steps(step, a.steps, lambda: torch.cuda.synchronize(dev), dist, red_dev)
-        lib.bertx_set_profiling(ctx, 0)
+        lib.bertx_set_profiling(model.ctx, 0)
         stats = model.kernel_stats()
 
     ms_per_step = elapsed / a.steps * 1e3
@@ -197,10 +312,14 @@ def main():
         "value": round(value, 2), "unit": "sentences/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "f16", "data": "synthetic (random-init weights, seeded token ids)",
-        "config": {"workload": f"{a.arch} {a.ftype} seq_len {L}, {B} sentences per GPU (bert_forward_batch path)",
+        "config": {"workload": f"{a.arch} {a.ftype} seq_len {L}, {B} sentences per GPU: bertx_forward_device on "
+                               f"HBM-resident token ids (the bert_forward_batch graph without its H2D/D2H)",
                    "batch_per_gpu": B, "global_batch": B * world, "seq_len": L, "weights": a.ftype,
                    "parallelism": f"replicas x{world} (no collectives)"},
-        "hbm_gbps_algorithmic": round(alg_bytes / (ms_per_step * 1e-3) / 1e9, 2),
+        # compulsory bytes (weights at stored width, gathered rows, ids, output) per
+        # step / step time: at C3 the path is MFMA-bound (AI ~1e5 FLOP/B), so this is
+        # NOT an HBM-roofline figure -- see probes.q4_0_hbm and roofline.traffic
+        "compulsory_gbps": round(alg_bytes / (ms_per_step * 1e-3) / 1e9, 2),
         "timing": "value: K graph-replayed forwards (no events); roofline/kernels: a second pass of K eager "
                   "forwards with HIP events around every kernel"
                   + ("" if a.no_profile else f" ({prof_elapsed / a.steps * 1e3:.3f} ms/step)"),
@@ -211,7 +330,10 @@ def main():
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         try:
             import oracle_lib
-            n_thr = min(16, os.cpu_count() or 1)
+            # the GPU box gives one GPU's job a 16-CPU share (OMP_NUM_THREADS=16 there;
+            # os.cpu_count() shows the whole machine): use every core of that share
+            share = len(os.sched_getaffinity(0))
+            n_thr = max(1, min(share, int(os.environ.get("OMP_NUM_THREADS", share))))
             orc = oracle_lib.Oracle(path)
             sample = [x for x in ids_list[: a.cpu_baseline_sentences]]
             c0 = time.perf_counter()
@@ -221,11 +343,19 @@ def main():
             res["cpu_baseline"] = {"value": round(len(sample) / (c1 - c0), 4), "unit": "sentences/s",
                                    "cores": n_thr, "kind": "port",
                                    "sample": f"{len(sample)} of the {B} sentences (L={L}) through the C oracle "
-                                             f"(oracle/bert_oracle.c, ggml-era q8 activation path), "
+                                             f"(oracle/bert_oracle.c, ggml-era q8 activation path) on {n_thr} "
+                                             f"threads = this job's CPU share ({share} CPUs visible, "
+                                             f"OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')}), "
                                              f"{c1 - c0:.1f} s",
                                    "gpu_vs_cpu_min_cosine": round(cos, 6)}
         except Exception as ex:  # the baseline is a report, never the product
             res["cpu_baseline"] = {"value": None, "error": str(ex)}
+
+    if rank == 0 and world == 1 and not a.no_probes:
+        try:
+            res["probes"] = probes(lib, bertpy, torch, a, dev, stream, path)
+        except Exception as ex:   # a probe is a report, never the metric
+            res["probes"] = {"error": str(ex)}
 
     if rank == 0:
         print(json.dumps(res), flush=True)

@@ -251,28 +251,60 @@ def synthetic_vocab(n_vocab):
     return v[:n_vocab]
 
 
-def synthetic_tensors(hp, seed=1234):
-    """Random weights per SURVEY.md §8d: matrices and biases N(0, 0.02), LN gamma 1+N(0,0.02),
-    beta N(0, 0.02), numpy default_rng(seed)."""
+def outlier_channels(d, seed=1234):
+    """The residual-stream channels the "sharp" profile drives to |x| ~ 50-200."""
+    return np.sort(np.random.default_rng(seed + 1).choice(d, 3, replace=False))
+
+
+def synthetic_tensors(hp, seed=1234, profile="survey"):
+    """Random weights, numpy default_rng(seed).
+
+    profile "survey" (the bench's weights): matrices and biases
+    N(0, 0.02), LN gamma 1+N(0,0.02), beta N(0, 0.02).  At that scale attention
+    is close to uniform, which hides key/value permutation and masking errors.
+
+    profile "sharp" (parity tests at full size, tuned on a float64 forward so that
+    rows stay distinct through every layer): LN gamma 4*(1+N(0,0.3)), Q/K matrices
+    N(0, 0.05) -- softmax rows are peaked (mean max-probability 0.1-0.5 per layer),
+    so the attention kernel's offset/rescale path runs and a key permutation or
+    mask error shows -- other matrices N(0, 0.02), embedding tables N(0, 0.5), and
+    three residual outlier channels (`outlier_channels`) the way trained BERT/BGE
+    checkpoints have them: O-proj and FFN-down biases of +-30/60/90 there with LN
+    gains of 0.3, so the pre-LN (f16) residual stream reaches |x| ~ 100 on those
+    channels while they do not swamp the LayerNorm."""
     rng = np.random.default_rng(seed)
     d, f = hp["n_embd"], hp["n_intermediate"]
     shapes = {"word": (hp["n_vocab"], d), "pos": (hp["n_max_tokens"], d), "type": (2, d), "dd": (d, d),
               "fd": (f, d), "df": (d, f), "d": (d,), "f": (f,), "ln_w": (d,), "ln_b": (d,)}
+    sharp = profile == "sharp"
+    assert profile in ("survey", "sharp"), profile
+    oc = outlier_channels(d, seed) if sharp else None
     out = {}
     for name, role in tensor_names(hp["n_layer"]):
-        a = rng.standard_normal(shapes[role], dtype=np.float32) * np.float32(0.02)
+        s = np.float32(0.02)
+        if sharp and role in ("word", "pos", "type"):
+            s = np.float32(0.5)
+        if sharp and (".query." in name or ".key." in name) and role == "dd":
+            s = np.float32(0.05)
+        a = rng.standard_normal(shapes[role], dtype=np.float32) * s
         if role == "ln_w":
-            a += np.float32(1.0)
+            if sharp:
+                a = np.float32(4.0) * (np.float32(1.0) + a * np.float32(15.0))
+                a[oc] = np.float32(0.3)
+            else:
+                a += np.float32(1.0)
+        if sharp and role == "d" and name.endswith("output.dense.bias"):
+            a[oc] += np.float32([30.0, -60.0, 90.0]) * np.float32(min(1.0, d / 768))
         out[name] = a
     return out
 
 
-def synthetic_model(path, arch, ftype="q4_0", seed=1234, lib=None):
+def synthetic_model(path, arch, ftype="q4_0", seed=1234, lib=None, profile="survey"):
     """Write a random-init model of `arch` in `ftype`.  Quantized files follow
     run_conversions.sh:5-8: f32 -> f16 file -> quantize from the f16 values."""
     hp = ARCHS[arch] if isinstance(arch, str) else arch
     vocab = synthetic_vocab(hp["n_vocab"])
-    tensors = synthetic_tensors(hp, seed)
+    tensors = synthetic_tensors(hp, seed, profile)
     if ftype in ("f32", "f16"):
         write_model(path, hp, vocab, tensors, FTYPE[ftype])
         return path

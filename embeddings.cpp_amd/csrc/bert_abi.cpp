@@ -32,6 +32,7 @@ struct bert_ctx {
 namespace {
 
 constexpr int64_t kChunkTokens = 1 << 17;   // tokens per device forward (workspace bound)
+constexpr int kChunkSeqs = 4096;            // sentences per device forward (pool / output staging bound)
 
 std::vector<int> parse_device_list(int n_visible)
 {
@@ -98,7 +99,8 @@ int run_forward(bert_ctx *ctx, const int32_t *const *toks, const int32_t *lens, 
         while (i < mine.size()) {
             tp.clear(); lp.clear(); op.clear();
             int64_t tok = 0;
-            while (i < mine.size() && (tp.empty() || tok + lens[mine[i]] <= kChunkTokens)) {
+            while (i < mine.size() && (tp.empty() || (tok + lens[mine[i]] <= kChunkTokens &&
+                                                       (int)tp.size() < kChunkSeqs))) {
                 const int idx = mine[i++];
                 tp.push_back(toks[idx]); lp.push_back(lens[idx]); op.push_back(outs[idx]);
                 tok += lens[idx];
@@ -212,6 +214,9 @@ struct bert_ctx *bert_load_from_file(const char *fname)
         ctx->devices.push_back(std::move(d));
     }
     std::printf("bert_load_from_file: MI355X engine on %zu HIP device(s)\n", ctx->devices.size());
+    if (m.hp.ftype == emb::FMT_F32)
+        std::printf("bert_load_from_file: f32 file: linear weights run as f16 MFMA operands with f32 accumulation "
+                    "(the reference multiplies f32 x f32, bert.cpp:499-503)\n");
     return ctx.release();
 }
 
@@ -335,8 +340,8 @@ int32_t bertx_reserve(struct bert_ctx *ctx, int32_t slot, int32_t total_tokens, 
     if (slot < 0 || slot >= (int32_t)ctx->devices.size()) return -1;
     Device &D = *ctx->devices[(size_t)slot];
     std::lock_guard<std::mutex> lk(D.mutex());
-    (void)hipSetDevice(D.ordinal());
-    return D.reserve(total_tokens, n_seqs) ? 0 : -1;
+    emb::DeviceGuard g(D.ordinal());
+    return D.reserve(total_tokens, n_seqs, ctx->hp.n_max_tokens) ? 0 : -1;
 }
 
 int32_t bertx_forward_device(struct bert_ctx *ctx, int32_t slot, const int32_t *d_ids, const int32_t *d_cu,
@@ -346,7 +351,7 @@ int32_t bertx_forward_device(struct bert_ctx *ctx, int32_t slot, const int32_t *
     if (max_len > ctx->hp.n_max_tokens || max_len <= 0) return -4;
     Device &D = *ctx->devices[(size_t)slot];
     std::lock_guard<std::mutex> lk(D.mutex());
-    (void)hipSetDevice(D.ordinal());
+    emb::DeviceGuard g(D.ordinal());
     return D.forward(d_ids, d_cu, n_seqs, max_len, total_tokens, d_out, stream ? (hipStream_t)stream : D.stream());
 }
 

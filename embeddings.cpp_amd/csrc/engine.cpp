@@ -219,7 +219,9 @@ void repack_table(const HostTensor &t, Piece &qs, Piece &dpl, Piece &mpl)
 
 Device::Device(int ordinal, const HostModel &m) : ordinal_(ordinal), hp_(m.hp)
 {
-    if (hipSetDevice(ordinal) != hipSuccess || hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) {
+    DeviceGuard g(ordinal);
+    if (!g.ok() || hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&done_ev_, hipEventDisableTiming) != hipSuccess) {
         std::fprintf(stderr, "libbert: cannot initialise HIP device %d\n", ordinal);
         return;
     }
@@ -228,7 +230,8 @@ Device::Device(int ordinal, const HostModel &m) : ordinal_(ordinal), hp_(m.hp)
 
 Device::~Device()
 {
-    (void)hipSetDevice(ordinal_);
+    DeviceGuard g(ordinal_);
+    if (done_ev_ && any_forward_) (void)hipEventSynchronize(done_ev_);
     if (stream_) (void)hipStreamSynchronize(stream_);
     drop_graphs();
     for (auto &p : pending_) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
@@ -238,7 +241,20 @@ Device::~Device()
     if (h_ids_) (void)hipHostFree(h_ids_);
     if (h_cu_) (void)hipHostFree(h_cu_);
     if (h_out_) (void)hipHostFree(h_out_);
+    if (done_ev_) (void)hipEventDestroy(done_ev_);
     if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+void Device::order_after_last(hipStream_t s)
+{
+    if (any_forward_ && last_stream_ != s) (void)hipStreamWaitEvent(s, done_ev_, 0);
+}
+
+void Device::mark_done(hipStream_t s)
+{
+    (void)hipEventRecord(done_ev_, s);
+    last_stream_ = s;
+    any_forward_ = true;
 }
 
 void Device::upload(const HostModel &m)
@@ -337,13 +353,19 @@ void Device::upload(const HostModel &m)
     ok_ = true;
 }
 
-bool Device::reserve(int64_t tokens, int64_t seqs)
+bool Device::reserve(int64_t tokens, int64_t seqs, int max_len)
 {
-    if (tokens <= cap_tokens_ && seqs <= cap_seqs_) return true;
-    HIP_OK(hipSetDevice(ordinal_));
+    const int64_t pool_rows = seqs * pool_chunks(std::max(1, std::min(max_len, hp_.n_max_tokens)));
+    if (tokens <= cap_tokens_ && seqs <= cap_seqs_ && pool_rows <= cap_pool_) return true;
+    DeviceGuard g(ordinal_);
+    HIP_OK(g.status());
+    if (any_forward_) HIP_OK(hipEventSynchronize(done_ev_));   // the last forward may be on a caller stream
     HIP_OK(hipStreamSynchronize(stream_));
     const int64_t nt = std::max<int64_t>(align_up((size_t)std::max(tokens, cap_tokens_), 4096), 4096);
     const int64_t ns = std::max<int64_t>(align_up((size_t)std::max(seqs, cap_seqs_), 256), 256);
+    // pool partials [n_seqs][chunks][d]: sized by the sentences' own max_len, not
+    // n_max_tokens (a chunk of many short texts would otherwise reserve GBs)
+    const int64_t np = std::max<int64_t>(align_up((size_t)std::max(pool_rows, cap_pool_), 256), 256);
     const int64_t rows = nt + GEMM_BM + 256;   // padding rows for tile overrun (kernels read, never trust)
     const int64_t d = hp_.n_embd, f = hp_.n_intermediate;
     size_t off = 0;
@@ -351,14 +373,14 @@ bool Device::reserve(int64_t tokens, int64_t seqs)
     const size_t o_st = take(rows * 8), o_yh = take(rows * d * 2), o_xh = take(rows * d * 2);
     const size_t o_qkv = take(rows * 3 * d * 2), o_att = take(rows * d * 2), o_ffn = take(rows * f * 2);
     const size_t o_ids = take(rows * 4), o_cu = take((ns + 1) * 4), o_out = take(ns * d * 4);
-    const size_t o_pool = take((size_t)ns * pool_chunks(hp_.n_max_tokens) * d * 4);
+    const size_t o_pool = take((size_t)np * d * 4);
     const size_t o_cnt = take((size_t)(rows / 128 + 1) * 4);   // zero between launches (the last workgroup resets)
     drop_graphs();   // captured graphs hold the old workspace pointers
     if (ws_) { (void)hipFree(ws_); ws_ = nullptr; }
     if (h_ids_) { (void)hipHostFree(h_ids_); h_ids_ = nullptr; }
     if (h_cu_) { (void)hipHostFree(h_cu_); h_cu_ = nullptr; }
     if (h_out_) { (void)hipHostFree(h_out_); h_out_ = nullptr; }
-    cap_tokens_ = cap_seqs_ = 0;
+    cap_tokens_ = cap_seqs_ = cap_pool_ = 0;
     HIP_OK(hipMalloc((void **)&ws_, off));
     // on the replica's own (non-blocking) stream: a null-stream memset would not
     // be ordered before the forward that follows on stream_
@@ -374,6 +396,7 @@ bool Device::reserve(int64_t tokens, int64_t seqs)
     HIP_OK(hipHostMalloc((void **)&h_out_, ns * d * 4, hipHostMallocDefault));
     cap_tokens_ = nt;
     cap_seqs_ = ns;
+    cap_pool_ = np;
     return true;
 }
 
@@ -404,7 +427,7 @@ void Device::end(int cls, hipStream_t s, hipEvent_t a, double work)
 
 void Device::collect_stats()
 {
-    (void)hipSetDevice(ordinal_);
+    DeviceGuard g(ordinal_);
     for (auto &p : pending_) {
         (void)hipEventSynchronize(p.b);
         float ms = 0.f;
@@ -436,8 +459,17 @@ int Device::forward(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, int m
                     hipStream_t s)
 {
     if (!ok_) return -3;
-    if (T > cap_tokens_ || n_seqs > cap_seqs_) return -2;
+    if (T > cap_tokens_ || n_seqs > cap_seqs_ || (int64_t)n_seqs * pool_chunks(max_len) > cap_pool_) return -2;
     if (T <= 0 || n_seqs <= 0) return 0;
+    order_after_last(s);
+    const int rc = forward_ordered(d_ids, d_cu, n_seqs, max_len, T, d_out, s);
+    mark_done(s);
+    return rc;
+}
+
+int Device::forward_ordered(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, int max_len, int T, float *d_out,
+                            hipStream_t s)
+{
     // BERT_CHECK_FINITE=1: after every kernel, count non-finite outputs over the
     // valid rows and report the first kernel that produced any (diagnostics).
     static const bool check = [] { const char *e = std::getenv("BERT_CHECK_FINITE"); return e && *e == '1'; }();
@@ -586,8 +618,10 @@ int Device::forward_host(const int32_t *const *tokens, const int32_t *lens, int 
     int64_t T = 0;
     int max_len = 0;
     for (int i = 0; i < n; ++i) { T += lens[i]; max_len = std::max(max_len, (int)lens[i]); }
-    HIP_RC(hipSetDevice(ordinal_));
-    if (!reserve(T, n)) return -1;
+    DeviceGuard g(ordinal_);
+    HIP_RC(g.status());
+    if (!reserve(T, n, max_len)) return -1;
+    order_after_last(stream_);   // the previous forward may have run on a caller stream
     h_cu_[0] = 0;
     for (int i = 0; i < n; ++i) {
         std::memcpy(h_ids_ + h_cu_[i], tokens[i], sizeof(int32_t) * (size_t)lens[i]);

@@ -33,6 +33,27 @@ struct DevLayer {
     float *ln1_w = nullptr, *ln1_b = nullptr, *ln2_w = nullptr, *ln2_b = nullptr;
 };
 
+// Sets the calling thread's current HIP device for a scope and restores the
+// previous one on exit (library calls must not move a host application's device).
+class DeviceGuard {
+public:
+    explicit DeviceGuard(int ordinal)
+    {
+        if (hipGetDevice(&prev_) != hipSuccess) { (void)hipGetLastError(); prev_ = -1; }
+        st_ = prev_ == ordinal ? hipSuccess : hipSetDevice(ordinal);
+        if (prev_ == ordinal) prev_ = -1;
+    }
+    ~DeviceGuard() { if (prev_ >= 0) (void)hipSetDevice(prev_); }
+    DeviceGuard(const DeviceGuard &) = delete;
+    DeviceGuard &operator=(const DeviceGuard &) = delete;
+    bool ok() const { return st_ == hipSuccess; }
+    hipError_t status() const { return st_; }
+
+private:
+    int prev_ = -1;
+    hipError_t st_ = hipSuccess;
+};
+
 class Device {
 public:
     Device(int ordinal, const HostModel &m);
@@ -43,12 +64,17 @@ public:
     std::mutex &mutex() { return mu_; }
 
     // Grow the workspace so one forward of `tokens` packed tokens / `seqs`
-    // sentences fits (never called inside a timed forward).
-    bool reserve(int64_t tokens, int64_t seqs);
+    // sentences of at most `max_len` tokens fits (never called inside a timed
+    // forward).  Waits for the replica's last forward, on whatever stream it ran.
+    bool reserve(int64_t tokens, int64_t seqs, int max_len);
 
     // Device-resident forward (ids, cu, out on this GPU); async on `s`.  When
     // profiling is off and `s` is not the null stream, the launch sequence is
     // captured once per (pointers, shape, stream) into a HIP graph and replayed.
+    // The workspace is shared by every forward of the replica: a forward on a
+    // stream other than the previous forward's first waits (on the device) for
+    // that forward's completion event, so calls on different streams never
+    // overlap in the workspace.
     int forward(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, int max_len, int total_tokens, float *d_out,
                 hipStream_t s);
 
@@ -77,6 +103,10 @@ private:
         }
     };
     struct GraphEntry { GraphKey key; hipGraphExec_t exec; };
+    int forward_ordered(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, int max_len, int T, float *d_out,
+                        hipStream_t s);
+    void order_after_last(hipStream_t s);   // stream s waits for the last forward (any stream)
+    void mark_done(hipStream_t s);          // records the completion event of a forward on s
     int launch_all(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, int max_len, int T, float *d_out,
                    hipStream_t s, bool check);
     void drop_graphs();
@@ -102,7 +132,10 @@ private:
     int layout_ = 1;                // DevWeight::layout of the linear weights
 
     // workspace
-    int64_t cap_tokens_ = 0, cap_seqs_ = 0;
+    int64_t cap_tokens_ = 0, cap_seqs_ = 0, cap_pool_ = 0;   // cap_pool_: pool partial rows (seqs x chunks)
+    hipEvent_t done_ev_ = nullptr;          // completion of the last forward
+    hipStream_t last_stream_ = nullptr;     // ... and the stream it ran on
+    bool any_forward_ = false;
     char *ws_ = nullptr;
     uint16_t *yh_ = nullptr;        // pre-LN residual stream (f16)
     float2 *st_ = nullptr;          // (mean, 1/sigma) of its last LN

@@ -70,13 +70,17 @@ def test_batch_composition_invariance(quant_models):
 
 
 def test_fake_batch_and_forward(quant_models):
-    m = bertpy.BertModel(quant_models[("tiny32", "f16")])
+    """bert_forward_fake_batch and bert_forward against the oracle's restatements
+    (oracle_forward_fake_batch: bert.cpp:1151-1363; bert_forward = a batch of one,
+    bert.cpp:817-825), not against the HIP batch path."""
+    path = quant_models[("tiny32", "f16")]
+    m = bertpy.BertModel(path)
+    o = oracle_lib.Oracle(path)
     ids = ragged_ids(690, [4, 50, 128])
-    a = m.forward_batch(ids)
     b = m.forward_batch(ids, fake=True)
-    assert np.all(cosines(a, b) >= 1 - 1e-6)
+    assert np.all(cosines(b, o.forward_fake_batch(ids)) >= 1 - COS_TOL)
     one = m.forward(ids[1])
-    assert np.all(cosines(one[None], a[1:2]) >= 1 - 1e-6)
+    assert np.all(cosines(one[None], o.forward_batch(ids[1:2])) >= 1 - COS_TOL)
 
 
 def test_too_long_is_refused(quant_models):

@@ -1,0 +1,152 @@
+"""BASELINE-size parity of the HIP forward with the CPU oracle on "sharp" weights.
+
+The bench's weights (SURVEY §8d, N(0, 0.02)) make attention almost uniform, so a
+key permutation or a masking error barely moves the output.  These tests use
+bertpy.synthetic_tensors(profile="sharp"): peaked softmax rows in every layer,
+LN gains spread 4*(1+N(0,0.3)) and three residual outlier channels at |x| ~ 100
+in the f16 pre-LN residual stream (the regime where an f16 residual could fail).
+
+Every SURVEY §8 configuration runs at full shape on the GPU through the C ABI:
+C1 MiniLM f32 L32 B1, C2 MiniLM f16 L128 B32, C3 bge-base q4_0 L512 B64, C4
+bge-large q4_1 L512 B32 (one GPU's shard of 256 over 8), C5 bge-base-zh q8_0
+ragged 16..512 B128.  Eight sentences of each -- the shortest and the longest
+among them -- are compared with the oracle (oracle/bert_oracle.c, restating
+bert.cpp:827-1147) at the north-star tolerance (1e-3 cosine).  The reference's
+own q8 activation rounding moves sharp bge-base embeddings by up to 1.5e-4
+cosine against the same weights with f32 activations (oracle vs oracle), which
+is why the tolerance is not tighter.
+
+PARITY_LOG=<file>: each test appends {config, min_cos, n} as one JSON line.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import bertpy
+import oracle_lib
+
+pytestmark = pytest.mark.gpu
+
+COS_TOL = 1e-3
+N_THR = min(16, os.cpu_count() or 1)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _one_device():
+    os.environ.pop("BERT_HOST_ONLY", None)
+    os.environ["BERT_DEVICES"] = "0"
+
+
+@pytest.fixture(scope="module")
+def sharp_models(tmp_path_factory):
+    d = tmp_path_factory.mktemp("sharp")
+    cache = {}
+
+    def get(arch, ftype):
+        if (arch, ftype) not in cache:
+            p = str(d / f"{arch}-{ftype}-sharp.bin")
+            bertpy.synthetic_model(p, arch, ftype, seed=1234, profile="sharp")
+            cache[(arch, ftype)] = p
+        return cache[(arch, ftype)]
+    return get
+
+
+def cosines(a, b):
+    return np.sum(a * b, axis=1) / (np.linalg.norm(a, axis=1) * np.linalg.norm(b, axis=1))
+
+
+def record(cfg, c):
+    log = os.environ.get("PARITY_LOG")
+    print(cfg, "min cos vs oracle %.7f over %d sentences" % (float(np.min(c)), len(c)))
+    if log:
+        with open(log, "a") as f:
+            f.write(json.dumps({"config": cfg, "min_cos": float(np.min(c)), "n": int(len(c))}) + "\n")
+
+
+def pick8(lens):
+    """Eight indices: the shortest, the longest, and six spread over the batch."""
+    lens = np.asarray(lens)
+    idx = [int(np.argmin(lens)), int(np.argmax(lens))]
+    for i in np.linspace(0, len(lens) - 1, 8).astype(int):
+        if len(idx) < 8 and int(i) not in idx:
+            idx.append(int(i))
+    i = 0
+    while len(idx) < min(8, len(lens)):
+        if i not in idx:
+            idx.append(i)
+        i += 1
+    return idx
+
+
+SHARP_CONFIGS = {
+    "C2-MiniLM-f16-L128-B32": ("all-MiniLM-L6-v2", "f16", [128] * 32),
+    "C3-bge-base-q4_0-L512-B64": ("bge-base-en-v1.5", "q4_0", [512] * 64),
+    "C4-bge-large-q4_1-L512-B32-shard": ("bge-large-en-v1.5", "q4_1", [512] * 32),
+    "C5-bge-base-zh-q8_0-ragged-B128": ("bge-base-zh-v1.5", "q8_0",
+                                        [int(x) for x in np.random.default_rng(11).integers(16, 513, 128)]),
+}
+
+
+@pytest.mark.parametrize("cfg", list(SHARP_CONFIGS))
+def test_sharp_config_matches_oracle(sharp_models, cfg):
+    arch, ftype, lens = SHARP_CONFIGS[cfg]
+    hp = bertpy.ARCHS[arch]
+    path = sharp_models(arch, ftype)
+    m = bertpy.BertModel(path)
+    ids = bertpy.synthetic_ids(len(lens), lens, hp["n_vocab"], seed=7)
+    full = m.forward_batch(ids)
+    assert np.all(np.isfinite(full))
+    assert np.allclose(np.linalg.norm(full, axis=1), 1.0, atol=1e-5)
+    check = pick8(lens)
+    sub = m.forward_batch([ids[i] for i in check])
+    assert np.array_equal(sub, full[check])          # batch-composition invariance
+    ref = oracle_lib.Oracle(path).forward_batch([ids[i] for i in check], n_threads=N_THR)
+    c = cosines(full[check], ref)
+    record(cfg, c)
+    assert np.all(c >= 1 - COS_TOL), c
+    # the sentences differ from each other (sharp weights: no collapse to one vector)
+    g = full[check] @ full[check].T
+    assert np.max(g[~np.eye(len(check), dtype=bool)]) < 0.999
+
+
+def test_sharp_c1_minilm_f32_single(sharp_models):
+    """C1: all-MiniLM-L6-v2 f32, L = 32, B = 1 (bert_forward, a batch of one), plus
+    seven more single-sentence calls of lengths 1..32."""
+    path = sharp_models("all-MiniLM-L6-v2", "f32")
+    m = bertpy.BertModel(path)
+    o = oracle_lib.Oracle(path)
+    lens = [32, 1, 2, 5, 16, 31, 3, 32]
+    ids = bertpy.synthetic_ids(len(lens), lens, 30522, seed=7)
+    got = np.stack([m.forward(x) for x in ids])
+    ref = np.concatenate([o.forward_batch([x], n_threads=N_THR) for x in ids])
+    c = cosines(got, ref)
+    record("C1-MiniLM-f32-L32-B1", c)
+    assert np.all(c >= 1 - COS_TOL), c
+
+
+def test_sharp_fake_batch_matches_oracle(sharp_models):
+    """bert_forward_fake_batch (bert.cpp:1151-1363: one graph per sentence, no mask,
+    pool 1/N, scale by 1/|e|) against the oracle's restatement of that path
+    (oracle_forward_fake_batch), and its write pattern when an input is too long:
+    the sentences before the first over-long one are written, the rest are not."""
+    path = sharp_models("bge-base-zh-v1.5", "q8_0")
+    m = bertpy.BertModel(path)
+    o = oracle_lib.Oracle(path)
+    lens = [16, 512, 77, 300, 2, 129, 450, 33]
+    ids = bertpy.synthetic_ids(len(lens), lens, 21128, seed=9)
+    got = m.forward_batch(ids, fake=True)
+    ref = o.forward_fake_batch(ids, n_threads=N_THR)
+    c = cosines(got, ref)
+    record("fake-batch-bge-base-zh-q8_0", c)
+    assert np.all(c >= 1 - COS_TOL), c
+    one = m.forward(ids[3])                          # bert_forward: a batch of one
+    assert cosines(one[None], ref[3:4])[0] >= 1 - COS_TOL
+    long_ = ids[:3] + [np.full(513, 1000, np.int32)] + ids[3:5]
+    out = m.forward_batch(long_, fake=True, fill=7.0)
+    assert not np.any(out[:3] == 7.0)
+    assert np.all(out[3:] == 7.0)
+    assert o.forward_fake_batch(long_, n_threads=N_THR) is None    # the oracle refuses too
+    assert np.array_equal(out[:3], got[:3])
+
