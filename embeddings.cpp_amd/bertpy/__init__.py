@@ -265,7 +265,8 @@ def synthetic_tensors(hp, seed=1234, profile="survey"):
 
     profile "sharp" (parity tests at full size, tuned on a float64 forward so that
     rows stay distinct through every layer): LN gamma 4*(1+N(0,0.3)), Q/K matrices
-    N(0, 0.05) -- softmax rows are peaked (mean max-probability 0.1-0.5 per layer),
+    N(0, 0.05) (N(0, 0.02) past 12 layers) -- softmax rows are peaked (mean
+    max-probability 0.1-0.9 per layer),
     so the attention kernel's offset/rescale path runs and a key permutation or
     mask error shows -- other matrices N(0, 0.02), embedding tables N(0, 0.5), and
     three residual outlier channels (`outlier_channels`) the way trained BERT/BGE
@@ -279,13 +280,17 @@ def synthetic_tensors(hp, seed=1234, profile="survey"):
     sharp = profile == "sharp"
     assert profile in ("survey", "sharp"), profile
     oc = outlier_channels(d, seed) if sharp else None
+    # Q/K spread: 24 layers of peaked attention amplify the reference's own q8
+    # activation rounding (bge-large at 0.05: oracle vs the same oracle with f32
+    # activations 0.88 cosine; at 0.02: >= 0.99966, the 3-token sentence worst)
+    qk_std = np.float32(0.05 if hp["n_layer"] <= 12 else 0.02)
     out = {}
     for name, role in tensor_names(hp["n_layer"]):
         s = np.float32(0.02)
         if sharp and role in ("word", "pos", "type"):
             s = np.float32(0.5)
         if sharp and (".query." in name or ".key." in name) and role == "dd":
-            s = np.float32(0.05)
+            s = qk_std
         a = rng.standard_normal(shapes[role], dtype=np.float32) * s
         if role == "ln_w":
             if sharp:

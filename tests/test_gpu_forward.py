@@ -190,3 +190,55 @@ def test_survey_config(tmp_path, cfg):
     c = cosines(full[check], ref)
     print(cfg, "min cos vs oracle", c.min())
     assert np.all(c >= 1 - COS_TOL), c
+
+
+def _hip():
+    """The HIP runtime libbert.so is linked against (libamdhip64.so.7 of /opt/rocm), by
+    soname: the process already holds it, so this is the same runtime instance (torch
+    bundles another one, which cannot share streams or pointers with it)."""
+    import ctypes
+    h = ctypes.CDLL("libamdhip64.so.7")
+    vp = ctypes.c_void_p
+    h.hipStreamCreate.argtypes = [ctypes.POINTER(vp)]
+    h.hipMalloc.argtypes = [ctypes.POINTER(vp), ctypes.c_size_t]
+    h.hipMemcpy.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_int]
+    h.hipStreamSynchronize.argtypes = [vp]
+    h.hipFree.argtypes = [vp]
+    h.hipStreamDestroy.argtypes = [vp]
+    return h
+
+
+def test_device_forward_on_caller_stream_is_ordered_before_host_forward(quant_models):
+    """bertx_forward_device enqueues on the caller's stream and returns; a following
+    bert_forward_batch (replica stream) must not overwrite the shared workspace
+    while that forward is in flight (engine.cpp order_after_last / mark_done)."""
+    import ctypes
+    hip = _hip()
+    path = quant_models[("tiny64", "q4_0")]
+    m = bertpy.BertModel(path)
+    ids = ragged_ids(690, [512, 300, 512, 129, 512, 77])
+    other = ragged_ids(690, [511, 2, 400], seed=9)
+    want = m.forward_batch(ids)
+    want_other = m.forward_batch(other)
+    flat = np.ascontiguousarray(np.concatenate(ids).astype(np.int32))
+    cu = np.concatenate([[0], np.cumsum([len(x) for x in ids])]).astype(np.int32)
+    T, B = int(cu[-1]), len(ids)
+    d_ids, d_cu, d_out, s = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+    assert hip.hipMalloc(ctypes.byref(d_ids), flat.nbytes) == 0
+    assert hip.hipMalloc(ctypes.byref(d_cu), cu.nbytes) == 0
+    assert hip.hipMalloc(ctypes.byref(d_out), B * m.n_embd * 4) == 0
+    assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+    assert hip.hipMemcpy(d_ids, flat.ctypes.data, flat.nbytes, 1) == 0     # H2D
+    assert hip.hipMemcpy(d_cu, cu.ctypes.data, cu.nbytes, 1) == 0
+    assert m.lib.bertx_reserve(m.ctx, 0, T, B) == 0
+    out = np.zeros((B, m.n_embd), np.float32)
+    for _ in range(3):                               # eager, then captured, then replayed
+        assert m.lib.bertx_forward_device(m.ctx, 0, d_ids, d_cu, B, 512, T, d_out, s) == 0
+        got_other = m.forward_batch(other)          # replica stream, issued while s may still run
+        assert hip.hipStreamSynchronize(s) == 0
+        assert hip.hipMemcpy(out.ctypes.data, d_out, out.nbytes, 2) == 0   # D2H
+        assert np.array_equal(out, want)
+        assert np.array_equal(got_other, want_other)
+    for p in (d_ids, d_cu, d_out):
+        hip.hipFree(p)
+    hip.hipStreamDestroy(s)

@@ -13,8 +13,10 @@ ragged 16..512 B128.  Eight sentences of each -- the shortest and the longest
 among them -- are compared with the oracle (oracle/bert_oracle.c, restating
 bert.cpp:827-1147) at the north-star tolerance (1e-3 cosine).  The reference's
 own q8 activation rounding moves sharp bge-base embeddings by up to 1.5e-4
-cosine against the same weights with f32 activations (oracle vs oracle), which
-is why the tolerance is not tighter.
+cosine against the same weights with f32 activations (oracle vs oracle), and
+3.4e-4 on a 3-token bge-large sentence, which is why the tolerance is not
+tighter (bge-large's Q/K spread is lower: at the bge-base value 24 peaked layers
+make the reference disagree with itself at 0.88 cosine).
 
 PARITY_LOG=<file>: each test appends {config, min_cos, n} as one JSON line.
 """
@@ -68,7 +70,9 @@ def record(cfg, c):
 def pick8(lens):
     """Eight indices: the shortest, the longest, and six spread over the batch."""
     lens = np.asarray(lens)
-    idx = [int(np.argmin(lens)), int(np.argmax(lens))]
+    idx = [int(np.argmin(lens))]
+    if int(np.argmax(lens)) not in idx:
+        idx.append(int(np.argmax(lens)))
     for i in np.linspace(0, len(lens) - 1, 8).astype(int):
         if len(idx) < 8 and int(i) not in idx:
             idx.append(int(i))
