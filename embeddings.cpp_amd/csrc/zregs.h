@@ -1,0 +1,139 @@
+// Lane-order weight fragments (kernels.h layout 1) for the 16x16x32 f16 MFMA
+// kernels (gemm16.hip): one lane's raw words of one K-step (64 k,
+// fragments u = 2a + s: features +16a, k-slice s) and their dequantization to
+// f16 A fragments, (q - 8) d (q4_0), q d + m (q4_1), q d (q8_0) rounded once;
+// and the permlane16 row exchange of the epilogues.
+#pragma once
+
+#include "device_common.h"
+#include "host_common.h"
+
+namespace emb {
+namespace {
+
+constexpr int ZK = 64;   // K per step (two k-slices of 32)
+
+__device__ __forceinline__ uint4 zload16(const void *p) { return *(const uint4 *)p; }
+__device__ __forceinline__ uint2 zload8(const void *p) { return *(const uint2 *)p; }
+typedef uint32_t zu32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t zu32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void zpin(uint4 &q)
+{
+    zu32x4 v = __builtin_bit_cast(zu32x4, q);
+    asm volatile("" : "+v"(v));
+    q = __builtin_bit_cast(uint4, v);
+}
+__device__ __forceinline__ void zpin(uint2 &q)
+{
+    zu32x2 v = __builtin_bit_cast(zu32x2, q);
+    asm volatile("" : "+v"(v));
+    q = __builtin_bit_cast(uint2, v);
+}
+
+__device__ __forceinline__ h16 zh(uint2 v, int u)   // f16 number u (0..3) of an 8-byte word pair
+{
+    const uint32_t w = u < 2 ? v.x : v.y;
+    return as_h((uint16_t)((u & 1) ? (w >> 16) : (w & 0xffffu)));
+}
+
+// One K-step of one lane's weight words: fragment (a, s) = features +16a,
+// k-slice s (block 2ks+s), index u = 2a + s.
+template <int FMT>
+struct ZRegs;
+
+template <int FMT>
+struct ZRegsQ4 {
+    uint4 q;           // word u: 8 nibbles, element i at bit 4*(i/2) + 16*(i%2)
+    uint2 d, m;        // f16 scale (and min) of fragment u
+    static constexpr int LOADS = FMT == FMT_Q4_1 ? 3 : 2;
+    static constexpr int QB = 16;
+    __device__ void load(const uint8_t *pq, const uint16_t *pd, const uint16_t *pm)
+    {
+        q = zload16(pq);
+        d = zload8(pd);
+        if (FMT == FMT_Q4_1) m = zload8(pm);
+    }
+    __device__ void pin_all() { zpin(q); zpin(d); if (FMT == FMT_Q4_1) zpin(m); }
+    __device__ h16x8 frag(int u) const
+    {
+        const uint32_t w = u == 0 ? q.x : u == 1 ? q.y : u == 2 ? q.z : q.w;
+        const h16 dh = zh(d, u);
+        const h16x2 d2 = {dh, dh};
+        h16x2 m2 = {(h16)0.0f, (h16)0.0f};
+        if (FMT == FMT_Q4_1) { const h16 mh = zh(m, u); m2 = h16x2{mh, mh}; }
+        const h16 o = FMT == FMT_Q4_1 ? (h16)-1024.0f : (h16)-1032.0f;
+        const h16x2 off = {o, o};
+        h16x8 a;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            h16x2 hh = as_h2(and_or_vs(w >> (4 * p), 0x000F000Fu, 0x64006400u)) + off;
+            hh = FMT == FMT_Q4_1 ? hh * d2 + m2 : hh * d2;
+            a[2 * p] = hh[0];
+            a[2 * p + 1] = hh[1];
+        }
+        return a;
+    }
+};
+template <> struct ZRegs<FMT_Q4_0> : ZRegsQ4<FMT_Q4_0> {};
+template <> struct ZRegs<FMT_Q4_1> : ZRegsQ4<FMT_Q4_1> {};
+
+template <>
+struct ZRegs<FMT_Q8_0> {
+    uint4 q0, q1;      // 8 bytes per fragment u at 8u: (q ^ 0x80), order e0 e2 e1 e3 per 4-group
+    uint2 d;
+    static constexpr int LOADS = 3;
+    static constexpr int QB = 32;
+    __device__ void load(const uint8_t *pq, const uint16_t *pd, const uint16_t *)
+    {
+        q0 = zload16(pq);
+        q1 = zload16(pq + 16);
+        d = zload8(pd);
+    }
+    __device__ void pin_all() { zpin(q0); zpin(q1); zpin(d); }
+    __device__ h16x8 frag(int u) const
+    {
+        const uint32_t w0 = u == 0 ? q0.x : u == 1 ? q0.z : u == 2 ? q1.x : q1.z;
+        const uint32_t w1 = u == 0 ? q0.y : u == 1 ? q0.w : u == 2 ? q1.y : q1.w;
+        const h16 dh = zh(d, u);
+        const h16x2 d2 = {dh, dh};
+        const h16x2 off = {(h16)-1152.0f, (h16)-1152.0f};
+        h16x8 a;
+        const h16x2 p0 = (as_h2((w0 & 0x00FF00FFu) | 0x64006400u) + off) * d2;
+        const h16x2 p1 = (as_h2(((w0 >> 8) & 0x00FF00FFu) | 0x64006400u) + off) * d2;
+        const h16x2 p2 = (as_h2((w1 & 0x00FF00FFu) | 0x64006400u) + off) * d2;
+        const h16x2 p3 = (as_h2(((w1 >> 8) & 0x00FF00FFu) | 0x64006400u) + off) * d2;
+        a[0] = p0[0]; a[1] = p0[1]; a[2] = p1[0]; a[3] = p1[1];
+        a[4] = p2[0]; a[5] = p2[1]; a[6] = p3[0]; a[7] = p3[1];
+        return a;
+    }
+};
+
+template <>
+struct ZRegs<FMT_F16> {
+    uint4 q[4];        // fragment u: 8 f16
+    static constexpr int LOADS = 4;
+    static constexpr int QB = 64;
+    __device__ void load(const uint8_t *pq, const uint16_t *, const uint16_t *)
+    {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) q[i] = zload16(pq + 16 * i);
+    }
+    __device__ void pin_all()
+    {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) zpin(q[i]);
+    }
+    __device__ h16x8 frag(int u) const { return __builtin_bit_cast(h16x8, q[u]); }
+};
+
+// v_permlane16_swap_b32 x, y: rows (16 lanes) 1 and 3 of x trade places with rows
+// 0 and 2 of y.  Inline asm: this compiler drops the builtin's second result
+// (it reuses the first -- seen in the emitted code), and the asm needs the
+// VALU-write -> permlane hazard's two wait states (s_nop 1) itself.
+__device__ __forceinline__ void zswap(float &x, float &y)
+{
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+}
+
+}  // namespace
+}  // namespace emb

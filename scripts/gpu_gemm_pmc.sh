@@ -1,0 +1,19 @@
+#!/bin/bash
+# PMC passes (one counter group per run) of one GEMM form for each tile config in CFGS
+set -o pipefail
+OUT=$GRAFT_REPO_ROOT/gpurun_out/${TAG:-gpmc}
+mkdir -p $OUT
+export TMPDIR=/tmp
+cd /tmp
+for cfg in ${CFGS:-0x1002 0x1006}; do
+  i=0
+  while read -r grp; do
+    [ -z "$grp" ] && continue
+    i=$((i+1))
+    timeout -s KILL 90 rocprofv3 --pmc $grp --output-format csv -d $OUT/${cfg}_p$i -o pmc -- python3 $GRAFT_REPO_ROOT/scripts/gemm_one.py ${CASE:-ffn_up} $cfg 10 > $OUT/${cfg}_p$i.log 2>&1 || exit $?
+  done <<GROUPS
+SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE
+SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_MFMA SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU
+GROUPS
+done
+echo done
