@@ -17,7 +17,7 @@ import struct
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-# BERT_LIB: an A/B build of the same library (scripts/build_variant.sh)
+# BERT_LIB: another build of the same library (A/B measurements)
 LIB_PATH = os.environ.get("BERT_LIB") or os.path.join(ROOT, "build", "libbert.so")
 
 FTYPE = {"f32": 0, "f16": 1, "q4_0": 2, "q4_1": 3, "q8_0": 8}
@@ -78,9 +78,9 @@ def load_lib(path=None):
     L.bertx_test_attention.argtypes = [vp, vp, c_i32, c_i32, c_i32, c_i32, vp]
     L.bertx_test_gemm.argtypes = [c_i32, c_i32, c_i32, vp, c_f32p, c_i32, vp, c_i32, vp, vp, c_i32]
     L.bertx_test_gemm_ln.restype = c_i32
-    L.bertx_test_gemm_ln.argtypes = [c_i32, c_i32, c_i32, vp, vp, c_i32, c_i32] + [vp] * 10 + [c_i32]
+    L.bertx_test_gemm_ln.argtypes = [c_i32, c_i32, c_i32, vp, vp, c_i32, vp, vp, vp, vp, c_i32] + [vp] * 7 + [c_i32]
     L.bertx_bench_gemm.restype = c_i32
-    L.bertx_bench_gemm.argtypes = [c_i32] * 8 + [c_f32p]
+    L.bertx_bench_gemm.argtypes = [c_i32] * 7 + [c_f32p]
     L.bertx_bench_attention.restype = c_i32
     L.bertx_bench_attention.argtypes = [c_i32] * 6 + [c_f32p]
     L.bertx_version.restype = ctypes.c_char_p

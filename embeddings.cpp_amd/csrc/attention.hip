@@ -161,13 +161,13 @@ __global__ __launch_bounds__(256) void attention_kernel(const h16 *__restrict__ 
 // K image chunk swizzle: the 16 lanes of a ds_read_b128 group read 16 rows
 // ({0-3,12-15,20-27} + 32n) at one chunk; XOR with (row >> 1) & 7 (128-B rows)
 // or (row >> 2) & 3 (64-B rows) puts them on 16 distinct 16-B bank slots.
-template <int CH, int VAR = 0>
+template <int CH>
 __device__ __forceinline__ int kswz(int row)
 {
     return CH == 8 ? ((row >> 1) & 7) : ((row >> 2) & 3);
 }
 
-template <int DH, int VAR = 0>
+template <int DH>
 __global__ __launch_bounds__(1024) void attention_lds_kernel(const h16 *__restrict__ qkv,
                                                              const int32_t *__restrict__ cu, int d, int nh,
                                                              float sl2, h16 *__restrict__ out)
@@ -191,7 +191,7 @@ __global__ __launch_bounds__(1024) void attention_lds_kernel(const h16 *__restri
         for (int i = w; i < ninstr; i += 16) {
             const int g = i * 64 + lane, row = g / CH, pc = g % CH;
             const int srow = min(row, len - 1);          // rows past the end: finite copies, masked / P = 0
-            const int ck = pc ^ kswz<CH, VAR>(row);
+            const int ck = pc ^ kswz<CH>(row);
             const int cv = pc ^ ((((row >> 1) & 1) << 2) & (CH - 1));
             glds<16>(kbase + (size_t)srow * ld + ck * 8, Kl + i * 1024);
             glds<16>(vbase + (size_t)srow * ld + cv * 8, Vl + i * 1024);
@@ -231,7 +231,7 @@ __global__ __launch_bounds__(1024) void attention_lds_kernel(const h16 *__restri
             const char *krow = Kl + row * RB;
 #pragma unroll
             for (int st = 0; st < DH / 16; ++st) {
-                const h16x8 a = *(const h16x8 *)(krow + (((2 * st + hi) ^ kswz<CH, VAR>(row)) << 4));
+                const h16x8 a = *(const h16x8 *)(krow + (((2 * st + hi) ^ kswz<CH>(row)) << 4));
                 s[kh] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, qf[st], s[kh], 0, 0, 0);
             }
         }
@@ -309,10 +309,10 @@ __global__ __launch_bounds__(1024) void attention_lds_kernel(const h16 *__restri
 }
 
 // ---------------------------------------------------------------------------
-// attention_lds2: the attention_lds structure (one workgroup per (sentence,
-// head), whole K/V in LDS, 16 waves x 32 queries, S^T = K Q^T with the query
-// on the lane) with the softmax VALU cut to the exp, the row sum and the f16
-// packing per score, and the K/V load overlapped with the first blocks:
+// attention_lds3 (production, dh 64) keeps the attention_lds structure (whole
+// K/V of a (sentence, head) in LDS, 16 waves x 32 queries, S^T = K Q^T with the
+// query on the lane) with the softmax VALU cut to the exp, the row sum and the
+// f16 packing per score:
 //  * fixed offset: each query keeps an f16 offset c (the max of its first
 //    block) and S - c comes out of the MFMA itself -- one extra MFMA per
 //    32 keys multiplies a ones-column of K by a (-c)-row of Q.  softmax(S) =
@@ -325,290 +325,14 @@ __global__ __launch_bounds__(1024) void attention_lds_kernel(const h16 *__restri
 //    halves are combined once, by v_permlane32_swap, at the end.
 //  * LDS reads at base + immediate offsets (the swizzles of both images are
 //    lane constants for 16-row-aligned blocks): six address adds per block.
-//  * K arrives first: the first block's Q K^T and softmax overlap V's DMA.
 // ---------------------------------------------------------------------------
-constexpr int ATT_SUMX = 12;
-
-__device__ __forceinline__ void swap32(float &a, float &b)
-{
-    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
-}
-// x over both 32-lane halves: lanes l and l ^ 32 combined
-__device__ __forceinline__ float halves_max(float x)
-{
-    float a = x, b = x;
-    swap32(a, b);
-    return fmaxf(a, b);
-}
-__device__ __forceinline__ float halves_sum(float x)
-{
-    float a = x, b = x;
-    swap32(a, b);
-    return a + b;
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vmcnt_upto(int n)   // s_waitcnt vmcnt(min(n, N)), n >= 0
-{
-    if constexpr (N == 0) wait_vmcnt<0>();
-    else {
-        if (n >= N) wait_vmcnt<N>();
-        else wait_vmcnt_upto<N - 1>(n);
-    }
-}
-
-// ABL (A/B diagnostics only): 1 = loads only, 2 = no K/V loads (compute on stale LDS),
-// 3 = stagger (waves w >= 4, 8, 12 start 320 cycles apart), 4 = s_setprio 1 around
-// the MFMA sections, 5 = K and V interleaved with one wait + stagger
-template <int ABL = 0>
-__global__ __launch_bounds__(1024) void attention_lds2_kernel(const h16 *__restrict__ qkv,
-                                                              const int32_t *__restrict__ cu, int d, int nh,
-                                                              float sl2, h16 *__restrict__ out)
-{
-    constexpr int DH = 64, RB = DH * 2, CH = RB / 16, LMAX = ATT_LDS_MAX;
-    __shared__ __attribute__((aligned(16))) char smem[2 * LMAX * RB];
-    char *Kl = smem;
-    const int h = blockIdx.x % nh, b = blockIdx.x / nh;
-    const int start = cu[b], len = cu[b + 1] - start;
-    if (len <= 0) return;
-    const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int hi = lane >> 5, lq = lane & 31;
-    const int ld = 3 * d;
-    const int nrows = (len + 63) & ~63;
-    const int q0 = 32 * w, q = q0 + lq;
-    const bool active = q0 < len && ABL != 1;             // wave-uniform
-
-    // Q rows first (older than the DMA, so every stage wait covers them)
-    h16x8 qf[DH / 16];
-    {
-        const h16 *qrow = qkv + (size_t)(start + min(q, len - 1)) * ld + h * DH;
-#pragma unroll
-        for (int s = 0; s < DH / 16; ++s) qf[s] = *(const h16x8 *)(qrow + 16 * s + 8 * hi);
-    }
-    // K and V -> LDS, 64 chunks of 16 B per wave-instruction; piece i = rows
-    // 8i .. 8i+7, wave w issues pieces w, w + 16, ... (stage j = pieces 16j ..
-    // 16j + 15 = rows 128j .. 128j + 127).  K swizzled by (row >> 1) & 7, V by
-    // ((row >> 1) & 1) << 2, via the source address; rows past the end are
-    // finite copies (masked / P = 0).
-    // ABL 5: pieces issued K, V interleaved, one wait; otherwise every K piece
-    // first, then every V piece: the first block's Q K^T and softmax run under V's DMA
-    constexpr bool SPLIT = ABL != 5;
-    int J = 0;                                            // this wave's pieces
-    {
-        const int ninstr = nrows * CH / 64;
-        const h16 *kbase = qkv + (size_t)start * ld + d + h * DH;
-        const h16 *vbase = kbase + d;
-        for (int i = w; i < ninstr; i += 16, ++J) {
-            const int g = i * 64 + lane, row = g / CH, pc = g % CH;
-            const size_t so = (size_t)min(row, len - 1) * ld;
-            if (ABL != 2) {
-                glds<16>(kbase + so + (pc ^ ((row >> 1) & 7)) * 8, Kl + i * 1024);
-                if (!SPLIT) glds<16>(vbase + so + (pc ^ (((row >> 1) & 1) << 2)) * 8, Kl + LMAX * RB + i * 1024);
-            }
-        }
-        if (SPLIT && ABL != 2)
-            for (int i = w; i < ninstr; i += 16) {
-                const int g = i * 64 + lane, row = g / CH, pc = g % CH;
-                const size_t so = (size_t)min(row, len - 1) * ld;
-                glds<16>(vbase + so + (pc ^ (((row >> 1) & 1) << 2)) * 8, Kl + LMAX * RB + i * 1024);
-            }
-    }
-    auto k_landed = [&]() {                               // every wave's K (and Q) pieces
-        if (SPLIT) wait_vmcnt_upto<4>(J);
-        else wait_vmcnt<0>();
-        __syncthreads();
-    };
-    auto v_landed = [&]() {                               // every wave's V pieces
-        if (SPLIT) {
-            wait_vmcnt<0>();
-            __syncthreads();
-        }
-    };
-    auto prio = [&](int p) {
-        if (ABL == 4) {
-            if (p) __builtin_amdgcn_s_setprio(1);
-            else __builtin_amdgcn_s_setprio(0);
-        }
-    };
-
-    // lane-constant LDS offsets (blocks are 64-row aligned)
-    int koff[DH / 16];
-#pragma unroll
-    for (int st = 0; st < DH / 16; ++st) koff[st] = lq * RB + (((2 * st + hi) ^ ((lq >> 1) & 7)) << 4);
-    const int gi = lane & 15, gq = gi >> 2, gp = gi & 3, gg = lane >> 4;
-    const int vsw = ((gq >> 1) & 1) << 2;
-    int voff[DH / 32];
-#pragma unroll
-    for (int t = 0; t < DH / 32; ++t) {
-        const int ch = 4 * t + 2 * (gg & 1) + (gp >> 1);
-        voff[t] = (4 * (gg >> 1) + gq) * RB + ((ch ^ vsw) << 4) + 8 * (gp & 1);
-    }
-    const h16 one = (h16)1.0f, zero = (h16)0.0f;
-    const h16x8 abias = {hi ? zero : one, zero, zero, zero, zero, zero, zero, zero};
-    h16x8 bbias = {zero, zero, zero, zero, zero, zero, zero, zero};
-
-    f32x16 o[DH / 32];
-#pragma unroll
-    for (int t = 0; t < DH / 32; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) o[t][r] = 0.f;
-    float c = 0.f, l = 0.f;                               // offset (f16-exact), this half's row sum
-    f32x16 s[2];
-
-    // per-block LDS bases pinned in VGPRs (the asm hides their constant parts,
-    // so every read is base + a 16-bit immediate offset)
-    auto qk = [&](int kb, bool bias) {
-        prio(1);
-        int kbo[DH / 16];
-#pragma unroll
-        for (int st = 0; st < DH / 16; ++st) {
-            kbo[st] = koff[st] + kb * RB;
-            asm volatile("" : "+v"(kbo[st]));
-        }
-#pragma unroll
-        for (int kh = 0; kh < 2; ++kh) {
-            if (bias) {
-                s[kh] = __builtin_amdgcn_mfma_f32_32x32x16_f16(abias, bbias, f32x16{}, 0, 0, 0);
-            } else {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) s[kh][r] = 0.f;
-            }
-#pragma unroll
-            for (int st = 0; st < DH / 16; ++st) {
-                const h16x8 a = *(const h16x8 *)(Kl + kbo[st] + kh * 32 * RB);
-                s[kh] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, qf[st], s[kh], 0, 0, 0);
-            }
-        }
-        prio(0);
-        if (kb + 64 > len) {
-#pragma unroll
-            for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int key = kb + 32 * kh + (r & 3) + 8 * (r >> 2) + 4 * hi;
-                    if (key >= len) s[kh][r] = -INFINITY;
-                }
-        }
-    };
-    auto row_max = [&]() {                                // over both halves
-        float mx = s[0][0];
-#pragma unroll
-        for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-            for (int r = (kh ? 0 : 1); r < 16; ++r) mx = fmaxf(mx, s[kh][r]);
-        return halves_max(mx);
-    };
-    auto shift_by = [&](float sh) {                       // scores -= sh
-#pragma unroll
-        for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) s[kh][r] -= sh;
-    };
-    auto expsum = [&]() {                                 // s <- exp2(s); this half's sum
-        float rs = 0.f;
-#pragma unroll
-        for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float p = __builtin_amdgcn_exp2f(s[kh][r]);
-                s[kh][r] = p;
-                rs += p;
-            }
-        return rs;
-    };
-    auto pv = [&](int kb) {
-        prio(1);
-        int vbo[DH / 32];
-#pragma unroll
-        for (int t = 0; t < DH / 32; ++t) {
-            vbo[t] = voff[t] + kb * RB + LMAX * RB;
-            asm volatile("" : "+v"(vbo[t]));
-        }
-#pragma unroll
-        for (int kh = 0; kh < 2; ++kh) {
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) {
-                h16x8 bp;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) bp[j] = (h16)s[kh][8 * s2 + j];
-#pragma unroll
-                for (int t = 0; t < DH / 32; ++t) {
-                    const char *va = smem + vbo[t] + (32 * kh + 16 * s2) * RB;
-                    const h16x4 lo = lds_read_tr16(va);
-                    const h16x4 up = lds_read_tr16(va + 8 * RB);
-                    const h16x8 a = {lo[0], lo[1], lo[2], lo[3], up[0], up[1], up[2], up[3]};
-                    o[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bp, o[t], 0, 0, 0);
-                }
-            }
-        }
-        prio(0);
-    };
-
-    k_landed();
-    if (ABL == 3 || ABL == 5) {
-        if (w >= 4) __builtin_amdgcn_s_sleep(5);
-        if (w >= 8) __builtin_amdgcn_s_sleep(5);
-        if (w >= 12) __builtin_amdgcn_s_sleep(5);
-    }
-    if (active) {
-        const h16 s16 = (h16)sl2;
-        const h16x8 sc = {s16, s16, s16, s16, s16, s16, s16, s16};
-#pragma unroll
-        for (int st = 0; st < DH / 16; ++st) qf[st] *= sc;
-        // first block: the offset is its row max (f16-rounded)
-        qk(0, false);
-        c = (float)(h16)row_max();
-        shift_by(c);
-        bbias[0] = hi ? zero : (h16)(-c);
-        l = expsum();
-    }
-    v_landed();
-    if (!active) return;                                  // no barrier follows
-    pv(0);
-    for (int kb = 64; kb < nrows; kb += 64) {
-        qk(kb, true);                                     // S - c
-        float rs = expsum();
-        if (__builtin_amdgcn_ballot_w64(rs > (float)(1 << ATT_SUMX))) {
-            // rare: move c to the row max, rescale, redo the block
-            qk(kb, true);
-            const float m = row_max();
-            const float sh = m > 0.f ? (float)(h16)(c + m) - c : 0.f;
-            const float alpha = __builtin_amdgcn_exp2f(-sh);
-            shift_by(sh);
-            c += sh;
-            bbias[0] = hi ? zero : (h16)(-c);
-            l *= alpha;
-#pragma unroll
-            for (int t = 0; t < DH / 32; ++t)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
-            rs = expsum();
-        }
-        l += rs;
-        pv(kb);
-    }
-
-    const float inv = 1.0f / halves_sum(l);
-    if (q < len) {
-        h16 *orow = out + (size_t)(start + q) * d + h * DH;
-#pragma unroll
-        for (int t = 0; t < DH / 32; ++t)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                h16x4 v;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = (h16)(o[t][4 * g + e] * inv);
-                *(h16x4 *)(orow + 32 * t + 8 * g + 4 * hi) = v;
-            }
-    }
-}
+constexpr int ATT_SUMX = 12;   // a block whose half-row sum passes 2^ATT_SUMX moves the offset
 
 // ---------------------------------------------------------------------------
-// attention_lds3 (production, dh 64): attention_lds2<4>'s arithmetic in a
-// persistent workgroup per CU that walks the items (sentence, head)
+// Persistence: one workgroup per CU that walks the items (sentence, head)
 // it = blockIdx.x, + gridDim.x, ..., so the K/V DMA of the next item runs
-// under the current item's MFMAs instead of in front of them (lds2 loads every
-// item in the open: about 16 of its 84 us at C3 were exposed loads).  The K/V
+// under the current item's MFMAs instead of in front of them (a workgroup per
+// item loads every item in the open: about 16 of 84 us at C3 were exposed loads).  The K/V
 // image is two regions of 256 keys (A = key blocks 0-3, B = blocks 4-7):
 //   B1 (every wave past the item's region-A blocks): the next item's region-A
 //      K/V pieces are issued;
@@ -651,7 +375,7 @@ __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restr
     // region r (rows 256 r .. 256 r + 255) of `it`: piece i = rows 8i .. 8i + 7;
     // wave w issues pieces 32 r + w and 32 r + w + 16 when they hold rows of the
     // sentence's 64-row blocks.  K swizzled by (row >> 1) & 7, V by
-    // ((row >> 1) & 1) << 2 (as attention_lds2); rows past the end are finite
+    // ((row >> 1) & 1) << 2 ; rows past the end are finite
     // copies (masked / P = 0).
     auto issue = [&](const Item &it, int r) {
         const int lane = lane_id_opaque();                // recomputed here: hoisted, its
@@ -785,7 +509,7 @@ __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restr
         __builtin_amdgcn_s_setprio(0);
     };
     // Q K^T and softmax of block kb > 0 (the first block, peeled off the block loop
-    // as in attention_lds2, sets the offset to its row max)
+    // sets the offset to its row max)
     auto scores = [&](int kb) {                           // blocks after the first
         qk(kb, true);                                     // S - c
         float rs = expsum();
@@ -915,31 +639,14 @@ void launch_attention(const uint16_t *qkv, const int32_t *cu, int32_t n_seqs, in
         const dim3 g(n_seqs * n_head), blk(1024);
         if (dh == 64) {
             // 0: production (attention_lds3, persistent, one workgroup per CU); 7:
-            // attention_lds3 on at most 7 workgroups (tests: many items each); 8:
-            // attention_lds2<4> (the previous production, MFMA sections at s_setprio 1);
-            // 1: attention_lds; 2..6: attention_lds2 A/B builds (ABL 0, 1, 2, 3, 5)
-            if (g_att_variant == 0 || g_att_variant == 7) {
-                const int n_items = n_seqs * n_head;
-                const int cap = g_att_variant == 7 ? 7 : att_cus();
-                const int grid = n_items < cap ? n_items : cap;
-                if (grid > 0)
-                    attention_lds3_kernel<<<grid, 1024, 0, s>>>((const h16 *)qkv, cu, d, n_head, n_items, sl2,
-                                                                (h16 *)out);
-                return;
-            }
-            decltype(&attention_lds2_kernel<0>) k = attention_lds2_kernel<4>;
-            switch (g_att_variant) {
-            case 1: k = attention_lds_kernel<64, 0>; break;
-            case 2: k = attention_lds2_kernel<0>; break;
-            case 3: k = attention_lds2_kernel<1>; break;
-            case 4: k = attention_lds2_kernel<2>; break;
-            case 5: k = attention_lds2_kernel<3>; break;
-            case 6: k = attention_lds2_kernel<5>; break;
-            default: break;
-            }
-            k<<<g, blk, 0, s>>>((const h16 *)qkv, cu, d, n_head, sl2, (h16 *)out);
+            // the same kernel on at most 7 workgroups (tests: many ragged items each)
+            const int n_items = n_seqs * n_head;
+            const int cap = g_att_variant == 7 ? 7 : att_cus();
+            const int grid = n_items < cap ? n_items : cap;
+            if (grid > 0)
+                attention_lds3_kernel<<<grid, 1024, 0, s>>>((const h16 *)qkv, cu, d, n_head, n_items, sl2, (h16 *)out);
         } else {
-            attention_lds_kernel<32, 0><<<g, blk, 0, s>>>((const h16 *)qkv, cu, d, n_head, sl2, (h16 *)out);
+            attention_lds_kernel<32><<<g, blk, 0, s>>>((const h16 *)qkv, cu, d, n_head, sl2, (h16 *)out);
         }
         return;
     }

@@ -382,7 +382,7 @@ int32_t bertx_kernel_stats(struct bert_ctx *ctx, int32_t idx, const char **name,
     if (total_ms) *total_ms = ms;
     if (work) *work = w;
     if (work_is_flops)
-        *work_is_flops = (idx == emb::K_EMBED_LN || idx == emb::K_LAYERNORM || idx == emb::K_POOL_L2) ? 0 : 1;
+        *work_is_flops = (idx == emb::K_EMBED_LN || idx == emb::K_LN_STATS || idx == emb::K_POOL_L2) ? 0 : 1;
     return 0;
 }
 

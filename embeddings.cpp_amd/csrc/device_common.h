@@ -21,6 +21,26 @@ __device__ __forceinline__ float wave_sum(float v)
     return v;
 }
 
+// v_permlane32_swap: lanes l and l ^ 32 of a and b trade places (the s_nop
+// covers the VALU-write -> permlane hazard the compiler does not see in asm)
+__device__ __forceinline__ void swap32(float &a, float &b)
+{
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+}
+// x combined over both 32-lane halves (lanes l and l ^ 32)
+__device__ __forceinline__ float halves_max(float x)
+{
+    float a = x, b = x;
+    swap32(a, b);
+    return fmaxf(a, b);
+}
+__device__ __forceinline__ float halves_sum(float x)
+{
+    float a = x, b = x;
+    swap32(a, b);
+    return a + b;
+}
+
 __device__ __forceinline__ h16x2 as_h2(uint32_t u) { return __builtin_bit_cast(h16x2, u); }
 __device__ __forceinline__ h16 as_h(uint16_t u) { return __builtin_bit_cast(h16, u); }
 // (x & vmask) | smagic as ONE v_and_or_b32: gfx9 VOP3 encodes no literal and reads at

@@ -12,8 +12,6 @@
 
 namespace emb {
 
-int g_weight_layout = 1;   // kernels.h
-
 #define HIP_OK(expr)                                                                                     \
     do {                                                                                                 \
         hipError_t e_ = (expr);                                                                          \
@@ -37,7 +35,7 @@ int g_weight_layout = 1;   // kernels.h
 const char *kclass_name(int k)
 {
     static const char *names[K_NUM_CLASSES] = {"embed_ln", "gemm_qkv", "attention", "gemm_attn_out",
-                                               "layernorm", "gemm_ffn_up", "gemm_ffn_down", "pool_l2"};
+                                               "ln_stats", "gemm_ffn_up", "gemm_ffn_down", "pool_l2"};
     return (k >= 0 && k < K_NUM_CLASSES) ? names[k] : "?";
 }
 
@@ -61,11 +59,15 @@ struct Piece {
     size_t off = 0;
 };
 
-// Linear weight [N][K] (file rows) -> K-step-major device layout (kernels.h).
-// Layout 1 (kernels.h, gemm16.hip): lane-order records per (K-step, 32-feature group).
-void repack_linear_l16(const std::vector<const HostTensor *> &parts, int fmt_dev, int N, int K, Piece &qs,
-                       Piece &dpl, Piece &mpl)
+// Linear weight [N][K] (file rows) -> the lane-order device layout (kernels.h).
+void repack_linear(const std::vector<const HostTensor *> &parts, int fmt_dev, Piece &qs, Piece &dpl, Piece &mpl,
+                   int &N_out, int &K_out)
 {
+    const int K = parts[0]->ne0;
+    int N = 0;
+    for (const HostTensor *t : parts) N += t->ne1;
+    N_out = N;
+    K_out = K;
     const size_t G = (size_t)N / 32;
     const size_t QB = fmt_dev == FMT_F16 ? 64 : fmt_dev == FMT_Q8_0 ? 32 : 16;
     qs.bytes.assign((size_t)(K / 64) * G * 64 * QB, 0);
@@ -74,7 +76,6 @@ void repack_linear_l16(const std::vector<const HostTensor *> &parts, int fmt_dev
     uint16_t *dd = (uint16_t *)dpl.bytes.data();
     uint16_t *mm = fmt_dev == FMT_Q4_1 ? (uint16_t *)mpl.bytes.data() : nullptr;
     static const int pos4[4] = {0, 2, 1, 3};
-    std::vector<float> row((size_t)K);
     int n = 0;
     for (const HostTensor *t : parts) {
         const size_t rb = fmt_row_bytes(t->fmt, K), bb = fmt_block_bytes(t->fmt);
@@ -115,79 +116,37 @@ void repack_linear_l16(const std::vector<const HostTensor *> &parts, int fmt_dev
     }
 }
 
-void repack_linear(const std::vector<const HostTensor *> &parts, int fmt_dev, Piece &qs, Piece &dpl, Piece &mpl,
-                   int &N_out, int &K_out, int layout)
+// LN fold constants (kernels.h) of a projection W (the concatenated parts) that
+// reads LN(y) = gamma (y - mean) r + beta: c1[n] = sum_k W[n][k] gamma[k],
+// c2[n] = b[n] + sum_k W[n][k] beta[k], with W as the GEMM multiplies it (each
+// weight rounded once to f16 after dequantization), summed in double.
+void fold_ln(const std::vector<const HostTensor *> &parts, const std::vector<const HostTensor *> &bias,
+             const HostTensor &gamma, const HostTensor &beta, Piece &c1, Piece &c2)
 {
     const int K = parts[0]->ne0;
-    int N = 0;
-    for (const HostTensor *t : parts) N += t->ne1;
-    N_out = N;
-    K_out = K;
-    if (layout == 1) {
-        repack_linear_l16(parts, fmt_dev, N, K, qs, dpl, mpl);
-        return;
-    }
-    const int KS = K / 64;
-    if (fmt_dev == FMT_F16) {
-        qs.bytes.assign((size_t)N * K * 2, 0);
-        uint16_t *dst = (uint16_t *)qs.bytes.data();
-        std::vector<float> row((size_t)K);
-        int n = 0;
-        for (const HostTensor *t : parts) {
-            const size_t rb = fmt_row_bytes(t->fmt, K);
-            for (int r = 0; r < t->ne1; ++r, ++n) {
-                const uint8_t *src = t->bytes.data() + rb * r;
-                for (int k = 0; k < K; ++k) {
-                    uint16_t h;
-                    if (t->fmt == FMT_F16) std::memcpy(&h, src + 2 * k, 2);
-                    else { float f; std::memcpy(&f, src + 4 * k, 4); h = f32_to_f16(f); }
-                    // A-fragment order (kernels.h): k = 16kk + 8hh + i -> 32hh + 8kk + i
-                    const int kr = k % 64, kk = kr / 16, hh = (kr / 8) & 1, i = kr % 8;
-                    dst[((size_t)(k / 64) * N + n) * 64 + 32 * hh + 8 * kk + i] = h;
-                }
-            }
-        }
-        return;
-    }
-    const size_t nblk = (size_t)N * (K / 32);
-    dpl.bytes.assign(nblk * 2, 0);
-    if (fmt_dev == FMT_Q4_1) mpl.bytes.assign(nblk * 2, 0);
-    qs.bytes.assign(nblk * (fmt_dev == FMT_Q8_0 ? 32 : 16), 0);
-    uint16_t *dd = (uint16_t *)dpl.bytes.data();
-    uint16_t *mm = fmt_dev == FMT_Q4_1 ? (uint16_t *)mpl.bytes.data() : nullptr;
-    int n = 0;
+    const float *gm = (const float *)gamma.bytes.data(), *bt = (const float *)beta.bytes.data();
+    std::vector<float> row((size_t)K), o1, o2;
     for (const HostTensor *t : parts) {
-        const size_t rb = fmt_row_bytes(t->fmt, K), bb = fmt_block_bytes(t->fmt);
-        for (int r = 0; r < t->ne1; ++r, ++n) {
-            for (int b = 0; b < K / 32; ++b) {
-                const uint8_t *blk = t->bytes.data() + rb * r + bb * b;
-                const size_t di = ((size_t)(b / 2) * N + n) * 2 + (b & 1);
-                (void)KS;
-                std::memcpy(&dd[di], blk, 2);
-                // element e of block b lands at k-slice kk = 2*(b&1) + e/16, lane half
-                // h = (e/8)&1, position i = e%8 of that (kk, h) fragment (kernels.h)
-                const size_t rec = (size_t)(b / 2) * N + n;
-                if (fmt_dev == FMT_Q8_0) {
-                    const int8_t *q = (const int8_t *)(blk + 2);
-                    uint8_t *o = qs.bytes.data() + rec * 64;
-                    static const int pos4[4] = {0, 2, 1, 3};
-                    for (int e = 0; e < 32; ++e) {
-                        const int kk = 2 * (b & 1) + e / 16, h = (e / 8) & 1, i = e % 8;
-                        o[32 * h + 8 * kk + 4 * (i / 4) + pos4[i % 4]] = (uint8_t)((uint8_t)q[e] ^ 0x80u);
-                    }
-                } else {
-                    const uint8_t *nib = blk + (fmt_dev == FMT_Q4_1 ? 4 : 2);
-                    if (mm) std::memcpy(&mm[di], blk + 2, 2);
-                    uint32_t *o = (uint32_t *)(qs.bytes.data() + rec * 32);
-                    for (int e = 0; e < 32; ++e) {
-                        const int kk = 2 * (b & 1) + e / 16, h = (e / 8) & 1, i = e % 8;
-                        const uint32_t q = e < 16 ? (nib[e] & 15u) : (uint32_t)(nib[e - 16] >> 4);
-                        o[4 * h + kk] |= q << (4 * (i / 2) + 16 * (i % 2));
-                    }
-                }
+        const size_t rb = fmt_row_bytes(t->fmt, K);
+        for (int r = 0; r < t->ne1; ++r) {
+            dequant_row(t->fmt, t->bytes.data() + rb * r, row.data(), K);
+            double s1 = 0.0, s2 = 0.0;
+            for (int k = 0; k < K; ++k) {
+                const double w = (double)f16_to_f32(f32_to_f16(row[(size_t)k]));
+                s1 += w * gm[k];
+                s2 += w * bt[k];
             }
+            o1.push_back((float)s1);
+            o2.push_back((float)s2);
         }
     }
+    size_t n = 0;
+    for (const HostTensor *b : bias) {
+        const float *bv = (const float *)b->bytes.data();
+        for (int i = 0; i < b->ne0; ++i, ++n) o2[n] = (float)((double)o2[n] + (double)bv[i]);
+    }
+    c1.bytes.assign((const uint8_t *)o1.data(), (const uint8_t *)(o1.data() + o1.size()));
+    c2.bytes.assign((const uint8_t *)o2.data(), (const uint8_t *)(o2.data() + o2.size()));
 }
 
 // Embedding table in its file format -> aligned planes.
@@ -267,19 +226,10 @@ void Device::upload(const HostModel &m)
         return;
     }
     wfmt_ = (hp_.ftype == FMT_F32 || hp_.ftype == FMT_F16) ? FMT_F16 : hp_.ftype;
-    {
-        const char *e = std::getenv("BERT_GEMM_LAYOUT");
-        layout_ = (e && (*e == '0' || *e == '1')) ? *e - '0' : g_weight_layout;
-    }
     std::vector<Piece> pieces;
     pieces.reserve(16 + 24 * (size_t)hp_.n_layer);
     auto add = [&](Piece &&p) -> size_t { pieces.push_back(std::move(p)); return pieces.size() - 1; };
     auto vec = [&](const HostTensor &t) -> size_t { Piece p; p.bytes = t.bytes; return add(std::move(p)); };
-    auto vec_cat = [&](std::initializer_list<const HostTensor *> ts) -> size_t {
-        Piece p;
-        for (const HostTensor *t : ts) p.bytes.insert(p.bytes.end(), t->bytes.begin(), t->bytes.end());
-        return add(std::move(p));
-    };
     struct TabIdx { size_t q, d, m; };
     auto table = [&](const HostTensor &t) -> TabIdx {
         Piece q, dd, mm;
@@ -292,13 +242,20 @@ void Device::upload(const HostModel &m)
     auto linear = [&](std::vector<const HostTensor *> parts) -> LinIdx {
         Piece q, dd, mm;
         LinIdx r;
-        repack_linear(parts, wfmt_, q, dd, mm, r.N, r.K, layout_);
+        repack_linear(parts, wfmt_, q, dd, mm, r.N, r.K);
         r.q = add(std::move(q)); r.d = add(std::move(dd)); r.m = add(std::move(mm));
         return r;
     };
     const TabIdx tw = table(m.word), tt = table(m.ttype), tp = table(m.pos);
     const size_t lnw = vec(m.ln_e_w), lnb = vec(m.ln_e_b);
-    struct LIdx { LinIdx qkv, o, up, down; size_t bqkv, bo, bup, bdown, l1w, l1b, l2w, l2b; };
+    auto fold = [&](std::vector<const HostTensor *> parts, std::vector<const HostTensor *> bias,
+                    const HostTensor &gamma, const HostTensor &beta, size_t &i1, size_t &i2) {
+        Piece c1, c2;
+        fold_ln(parts, bias, gamma, beta, c1, c2);
+        i1 = add(std::move(c1));
+        i2 = add(std::move(c2));
+    };
+    struct LIdx { LinIdx qkv, o, up, down; size_t bo, bdown, c1q, c2q, c1u, c2u, l1w, l1b, l2w, l2b; };
     std::vector<LIdx> li((size_t)hp_.n_layer);
     for (int l = 0; l < hp_.n_layer; ++l) {
         const HostLayer &L = m.layers[(size_t)l];
@@ -307,8 +264,12 @@ void Device::upload(const HostModel &m)
         x.o = linear({&L.o_w});
         x.up = linear({&L.i_w});
         x.down = linear({&L.o2_w});
-        x.bqkv = vec_cat({&L.q_b, &L.k_b, &L.v_b});
-        x.bo = vec(L.o_b); x.bup = vec(L.i_b); x.bdown = vec(L.o2_b);
+        // the LN in front of QKV: the previous layer's output LN, or the embedding LN
+        const HostTensor &gq = l ? m.layers[(size_t)l - 1].ln_out_w : m.ln_e_w;
+        const HostTensor &bq = l ? m.layers[(size_t)l - 1].ln_out_b : m.ln_e_b;
+        fold({&L.q_w, &L.k_w, &L.v_w}, {&L.q_b, &L.k_b, &L.v_b}, gq, bq, x.c1q, x.c2q);
+        fold({&L.i_w}, {&L.i_b}, L.ln_att_w, L.ln_att_b, x.c1u, x.c2u);
+        x.bo = vec(L.o_b); x.bdown = vec(L.o2_b);
         x.l1w = vec(L.ln_att_w); x.l1b = vec(L.ln_att_b); x.l2w = vec(L.ln_out_w); x.l2b = vec(L.ln_out_b);
     }
     size_t total = 0;
@@ -338,7 +299,7 @@ void Device::upload(const HostModel &m)
     ln_e_b_ = (float *)P(lnb);
     auto mk_lin = [&](const LinIdx &x) {
         DevWeight w;
-        w.fmt = wfmt_; w.N = x.N; w.K = x.K; w.layout = layout_;
+        w.fmt = wfmt_; w.N = x.N; w.K = x.K;
         w.qs = P(x.q); w.d = (const uint16_t *)P(x.d); w.m = (const uint16_t *)P(x.m);
         return w;
     };
@@ -347,7 +308,8 @@ void Device::upload(const HostModel &m)
         const LIdx &x = li[(size_t)l];
         DevLayer &D = layers_[(size_t)l];
         D.qkv = mk_lin(x.qkv); D.o = mk_lin(x.o); D.up = mk_lin(x.up); D.down = mk_lin(x.down);
-        D.b_qkv = (float *)P(x.bqkv); D.b_o = (float *)P(x.bo); D.b_up = (float *)P(x.bup); D.b_down = (float *)P(x.bdown);
+        D.b_o = (float *)P(x.bo); D.b_down = (float *)P(x.bdown);
+        D.c1_qkv = (float *)P(x.c1q); D.c2_qkv = (float *)P(x.c2q); D.c1_up = (float *)P(x.c1u); D.c2_up = (float *)P(x.c2u);
         D.ln1_w = (float *)P(x.l1w); D.ln1_b = (float *)P(x.l1b); D.ln2_w = (float *)P(x.l2w); D.ln2_b = (float *)P(x.l2b);
     }
     ok_ = true;
@@ -370,11 +332,10 @@ bool Device::reserve(int64_t tokens, int64_t seqs, int max_len)
     const int64_t d = hp_.n_embd, f = hp_.n_intermediate;
     size_t off = 0;
     auto take = [&](size_t bytes) { size_t o = off; off += align_up(bytes, 256); return o; };
-    const size_t o_st = take(rows * 8), o_yh = take(rows * d * 2), o_xh = take(rows * d * 2);
+    const size_t o_st = take(rows * 8), o_z = take(rows * d * 2), o_part = take(rows * (d / 32) * 8);
     const size_t o_qkv = take(rows * 3 * d * 2), o_att = take(rows * d * 2), o_ffn = take(rows * f * 2);
     const size_t o_ids = take(rows * 4), o_cu = take((ns + 1) * 4), o_out = take(ns * d * 4);
     const size_t o_pool = take((size_t)np * d * 4);
-    const size_t o_cnt = take((size_t)(rows / 128 + 1) * 4);   // zero between launches (the last workgroup resets)
     drop_graphs();   // captured graphs hold the old workspace pointers
     if (ws_) { (void)hipFree(ws_); ws_ = nullptr; }
     if (h_ids_) { (void)hipHostFree(h_ids_); h_ids_ = nullptr; }
@@ -386,11 +347,11 @@ bool Device::reserve(int64_t tokens, int64_t seqs, int max_len)
     // be ordered before the forward that follows on stream_
     HIP_OK(hipMemsetAsync(ws_, 0, off, stream_));
     HIP_OK(hipStreamSynchronize(stream_));
-    st_ = (float2 *)(ws_ + o_st); yh_ = (uint16_t *)(ws_ + o_yh); xh_ = (uint16_t *)(ws_ + o_xh);
+    st_ = (float2 *)(ws_ + o_st); z_ = (uint16_t *)(ws_ + o_z); part_ = (float2 *)(ws_ + o_part);
+    rows_ = rows;
     qkv_ = (uint16_t *)(ws_ + o_qkv); att_ = (uint16_t *)(ws_ + o_att); ffn_ = (uint16_t *)(ws_ + o_ffn);
     d_ids_ = (int32_t *)(ws_ + o_ids); d_cu_ = (int32_t *)(ws_ + o_cu); d_out_ = (float *)(ws_ + o_out);
     pool_part_ = (float *)(ws_ + o_pool);
-    panel_cnt_ = (uint32_t *)(ws_ + o_cnt);
     HIP_OK(hipHostMalloc((void **)&h_ids_, nt * 4, hipHostMallocDefault));
     HIP_OK(hipHostMalloc((void **)&h_cu_, (ns + 1) * 4, hipHostMallocDefault));
     HIP_OK(hipHostMalloc((void **)&h_out_, ns * d * 4, hipHostMallocDefault));
@@ -456,8 +417,11 @@ void Device::drop_graphs()
 }
 
 int Device::forward(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, int max_len, int T, float *d_out,
-                    hipStream_t s)
+                    hipStream_t s, double len2_sum)
 {
+    // attention work for the per-kernel stats: exact from the host's lengths when
+    // known, else T max_len (exact for equal lengths, an upper bound otherwise)
+    att_flop_ = 4.0 * hp_.n_embd * (len2_sum >= 0 ? len2_sum : (double)T * max_len);
     if (!ok_) return -3;
     if (T > cap_tokens_ || n_seqs > cap_seqs_ || (int64_t)n_seqs * pool_chunks(max_len) > cap_pool_) return -2;
     if (T <= 0 || n_seqs <= 0) return 0;
@@ -536,28 +500,22 @@ int Device::launch_all(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, in
     };
 
     begin(K_EMBED_LN, s, ev);
-    launch_embed_ln(word_, type_, pos_, ln_e_w_, ln_e_b_, d_ids, d_cu, n_seqs, max_len, d, yh_, xh_, st_, s);
-    end(K_EMBED_LN, s, ev, t * (4.0 + 3.0 * d * 2.0 + 6.0 * d));
-    chk("embed_ln", -1, xh_, (size_t)T * d, 1);
-    // the residual stream stays pre-LN; `prev` is the LN that normalises it
-    ResLN prev;
-    prev.stats = st_; prev.w = ln_e_w_; prev.b = ln_e_b_;
+    launch_embed_ln(word_, type_, pos_, ln_e_w_, d_ids, d_cu, n_seqs, max_len, d, z_, st_, s);
+    end(K_EMBED_LN, s, ev, t * (4.0 + 3.0 * d * 2.0 + 2.0 * d + 8.0));
+    chk("embed_ln", -1, z_, (size_t)T * d, 1);
+    // z_ holds the stream as z = y * gamma of the LN in front of the next
+    // projection, st_ its (mean, 1/sigma) (kernels.h LN fold); (gz, bz) is that LN
+    const float *gz = ln_e_w_, *bz = ln_e_b_;
+    const int G = d / 32;
 
-    const double att_flop = 4.0 * (double)d * t * (double)max_len;   // exact when all lengths are equal
-    // the residual GEMM may also run the LayerNorm that follows it (panel LN,
-    // kernels.h ResLN); launch_gemm says whether it did
-    auto panel = [&](const ResLN &in, const float *w, const float *b) {
-        ResLN r = in;
-        if (!panel_ln_ || check) return r;
-        r.cnt = panel_cnt_; r.xh = xh_; r.st_out = st_; r.nw = w; r.nb = b; r.rows = T;
-        static const int pvar = [] { const char *e = std::getenv("BERT_PANEL_VARIANT"); return e ? std::atoi(e) : 0; }();
-        r.pvar = pvar;
-        return r;
-    };
+    const double att_flop = att_flop_;   // sum over sentences of 4 d len^2 (QK^T and PV), set by the caller
     for (int l = 0; l < hp_.n_layer; ++l) {
         const DevLayer &L = layers_[(size_t)l];
+        LnFold in;
+        in.in_stats = st_;
+        in.c1 = L.c1_qkv;
         begin(K_GEMM_QKV, s, ev);
-        launch_gemm(L.qkv, xh_, M, L.b_qkv, EPI_BIAS_F16, nullptr, qkv_, s);
+        launch_gemm(L.qkv, z_, M, L.c2_qkv, EPI_BIAS_F16, nullptr, qkv_, s, in);
         end(K_GEMM_QKV, s, ev, 2.0 * t * 3.0 * d * d);
         chk("gemm_qkv", l, qkv_, (size_t)T * 3 * d, 1);
 
@@ -566,41 +524,42 @@ int Device::launch_all(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, in
         end(K_ATTENTION, s, ev, att_flop);
         chk("attention", l, att_, (size_t)T * d, 1);
 
+        // y1 = LN(y) + ATT W_o^T + b_o, stored as z = y1 * gamma_1 with its partials
+        LnFold r1;
+        r1.res_stats = st_; r1.res_g = gz; r1.res_b = bz;
+        r1.g_next = L.ln1_w; r1.part = part_; r1.part_stride = (int32_t)rows_;
         begin(K_GEMM_O, s, ev);
-        const int ln1_fused = launch_gemm(L.o, att_, M, L.b_o, EPI_BIAS_RES, yh_, yh_, s, panel(prev, L.ln1_w, L.ln1_b));
+        launch_gemm(L.o, att_, M, L.b_o, EPI_BIAS_RES, z_, z_, s, r1);
         end(K_GEMM_O, s, ev, 2.0 * t * d * d);
-        chk("gemm_o", l, yh_, (size_t)T * d, 1);
+        chk("gemm_o", l, z_, (size_t)T * d, 1);
 
-        if (!ln1_fused) {
-            begin(K_LAYERNORM, s, ev);
-            launch_layernorm(yh_, T, d, L.ln1_w, L.ln1_b, xh_, st_, s);
-            end(K_LAYERNORM, s, ev, t * d * 10.0);
-        }
-        prev.w = L.ln1_w; prev.b = L.ln1_b;
-        chk("layernorm1", l, xh_, (size_t)T * d, 1);
+        begin(K_LN_STATS, s, ev);
+        launch_ln_stats(part_, G, (int32_t)rows_, M, d, st_, s);
+        end(K_LN_STATS, s, ev, (double)M * (G + 1) * 8.0);
+        gz = L.ln1_w; bz = L.ln1_b;
 
+        in.c1 = L.c1_up;
         begin(K_GEMM_FFN_UP, s, ev);
-        launch_gemm(L.up, xh_, M, L.b_up, EPI_BIAS_GELU_F16, nullptr, ffn_, s);
+        launch_gemm(L.up, z_, M, L.c2_up, EPI_BIAS_GELU_F16, nullptr, ffn_, s, in);
         end(K_GEMM_FFN_UP, s, ev, 2.0 * t * d * f);
         chk("gemm_up", l, ffn_, (size_t)T * f, 1);
 
+        LnFold r2;
+        r2.res_stats = st_; r2.res_g = gz; r2.res_b = bz;
+        r2.g_next = L.ln2_w; r2.part = part_; r2.part_stride = (int32_t)rows_;
         begin(K_GEMM_FFN_DOWN, s, ev);
-        const int ln2_fused =
-            launch_gemm(L.down, ffn_, M, L.b_down, EPI_BIAS_RES, yh_, yh_, s, panel(prev, L.ln2_w, L.ln2_b));
+        launch_gemm(L.down, ffn_, M, L.b_down, EPI_BIAS_RES, z_, z_, s, r2);
         end(K_GEMM_FFN_DOWN, s, ev, 2.0 * t * d * f);
-        chk("gemm_down", l, yh_, (size_t)T * d, 1);
+        chk("gemm_down", l, z_, (size_t)T * d, 1);
 
-        if (!ln2_fused) {
-            begin(K_LAYERNORM, s, ev);
-            launch_layernorm(yh_, T, d, L.ln2_w, L.ln2_b, xh_, st_, s);
-            end(K_LAYERNORM, s, ev, t * d * 10.0);
-        }
-        prev.w = L.ln2_w; prev.b = L.ln2_b;
-        chk("layernorm2", l, xh_, (size_t)T * d, 1);
+        begin(K_LN_STATS, s, ev);
+        launch_ln_stats(part_, G, (int32_t)rows_, M, d, st_, s);
+        end(K_LN_STATS, s, ev, (double)M * (G + 1) * 8.0);
+        gz = L.ln2_w; bz = L.ln2_b;
     }
     begin(K_POOL_L2, s, ev);
-    launch_pool_l2(yh_, prev, d_cu, n_seqs, max_len, d, pool_part_, d_out, s);
-    end(K_POOL_L2, s, ev, t * d * 4.0 + (double)n_seqs * d * 4.0);
+    launch_pool_l2(z_, st_, gz, bz, d_cu, n_seqs, max_len, d, pool_part_, d_out, s);
+    end(K_POOL_L2, s, ev, t * d * 2.0 + t * 8.0 + (double)n_seqs * d * 4.0);
     chk("pool_l2", -1, d_out, (size_t)n_seqs * d, 0);
     if (cnt) (void)hipFree(cnt);
     const hipError_t e = hipGetLastError();
@@ -617,7 +576,12 @@ int Device::forward_host(const int32_t *const *tokens, const int32_t *lens, int 
     if (n <= 0) return 0;
     int64_t T = 0;
     int max_len = 0;
-    for (int i = 0; i < n; ++i) { T += lens[i]; max_len = std::max(max_len, (int)lens[i]); }
+    double len2 = 0.0;
+    for (int i = 0; i < n; ++i) {
+        T += lens[i];
+        max_len = std::max(max_len, (int)lens[i]);
+        len2 += (double)lens[i] * lens[i];
+    }
     DeviceGuard g(ordinal_);
     HIP_RC(g.status());
     if (!reserve(T, n, max_len)) return -1;
@@ -629,7 +593,7 @@ int Device::forward_host(const int32_t *const *tokens, const int32_t *lens, int 
     }
     HIP_RC(hipMemcpyAsync(d_ids_, h_ids_, sizeof(int32_t) * (size_t)T, hipMemcpyHostToDevice, stream_));
     HIP_RC(hipMemcpyAsync(d_cu_, h_cu_, sizeof(int32_t) * (size_t)(n + 1), hipMemcpyHostToDevice, stream_));
-    const int rc = forward(d_ids_, d_cu_, n, max_len, (int)T, d_out_, stream_);
+    const int rc = forward(d_ids_, d_cu_, n, max_len, (int)T, d_out_, stream_, len2);
     if (rc != 0) return rc;
     const size_t d = (size_t)hp_.n_embd;
     HIP_RC(hipMemcpyAsync(h_out_, d_out_, sizeof(float) * d * (size_t)n, hipMemcpyDeviceToHost, stream_));
@@ -641,282 +605,181 @@ int Device::forward_host(const int32_t *const *tokens, const int32_t *lens, int 
 }  // namespace emb
 
 // ---------------------------------------------------------------------------
-// per-kernel parity hook (bert_hip.h): one GEMM on device 0, host buffers
+// per-kernel parity hooks (bert_hip.h): one GEMM on device 0, host buffers
 // ---------------------------------------------------------------------------
 #include "bert_hip.h"
 
-extern "C" int32_t bertx_test_gemm(int32_t fmt, int32_t N, int32_t K, const void *w_rows, const float *bias,
-                                   int32_t M, const uint16_t *x, int32_t epi, const void *res, void *out,
-                                   int32_t tile_n)
+namespace emb {
+namespace {
+
+// Device buffers of one hook call, freed together.
+struct HookBufs {
+    std::vector<void *> p;
+    bool bad = false;
+    void *up(const void *h, size_t bytes, size_t alloc)
+    {
+        void *d = nullptr;
+        alloc = std::max<size_t>(std::max(alloc, bytes), 16);
+        if (hipMalloc(&d, alloc) != hipSuccess) { bad = true; return nullptr; }
+        p.push_back(d);
+        if (hipMemset(d, 0, alloc) != hipSuccess) bad = true;
+        if (h && bytes && hipMemcpy(d, h, bytes, hipMemcpyHostToDevice) != hipSuccess) bad = true;
+        return d;
+    }
+    ~HookBufs() { for (void *d : p) (void)hipFree(d); }
+};
+
+// The weight of a hook call in the device layout; t keeps the file-format rows.
+bool hook_weight(int32_t fmt, int32_t N, int32_t K, const void *w_rows, HostTensor &t, DevWeight &W, HookBufs &B)
 {
-    using namespace emb;
-    if (!fmt_valid(fmt) || K % 64 || N % 4 || M <= 0 || hip_device_count() == 0) return -1;
-    HostTensor t;
     t.fmt = fmt; t.ne0 = K; t.ne1 = N;
     t.bytes.assign((const uint8_t *)w_rows, (const uint8_t *)w_rows + fmt_row_bytes(fmt, K) * (size_t)N);
     const int fdev = (fmt == FMT_F32 || fmt == FMT_F16) ? FMT_F16 : fmt;
     Piece q, dd, mm;
-    int n_out = 0, k_out = 0;
-    // tile_n: 0 production; 128 / 256 gemm.hip tiles (layout 0); 0x1000 | cfg gemm16 (layout 1)
-    const int layout = tile_n == 0 ? g_weight_layout : (tile_n & 0x1000) ? 1 : 0;
-    repack_linear({&t}, fdev, q, dd, mm, n_out, k_out, layout);
+    repack_linear({&t}, fdev, q, dd, mm, W.N, W.K);
+    W.fmt = fdev;
+    W.qs = B.up(q.bytes.data(), q.bytes.size(), 0);
+    W.d = (const uint16_t *)(dd.bytes.empty() ? nullptr : B.up(dd.bytes.data(), dd.bytes.size(), 0));
+    W.m = (const uint16_t *)(mm.bytes.empty() ? nullptr : B.up(mm.bytes.data(), mm.bytes.size(), 0));
+    return !B.bad;
+}
+
+HostTensor vec_tensor(const float *v, int n)
+{
+    HostTensor t;
+    t.fmt = FMT_F32; t.ne0 = n; t.ne1 = 1;
+    t.bytes.assign((const uint8_t *)v, (const uint8_t *)(v + n));
+    return t;
+}
+
+}  // namespace
+}  // namespace emb
+
+extern "C" int32_t bertx_test_gemm(int32_t fmt, int32_t N, int32_t K, const void *w_rows, const float *bias,
+                                   int32_t M, const uint16_t *x, int32_t epi, const void *res, void *out,
+                                   int32_t cfg)
+{
+    return bertx_test_gemm_ln(fmt, N, K, w_rows, bias, M, x, nullptr, nullptr, nullptr, epi, (const uint16_t *)res,
+                              nullptr, nullptr, nullptr, nullptr, (uint16_t *)out, nullptr, cfg);
+}
+
+extern "C" int32_t bertx_test_gemm_ln(int32_t fmt, int32_t N, int32_t K, const void *w_rows, const float *bias,
+                                      int32_t M, const uint16_t *x, const float *in_stats, const float *in_g,
+                                      const float *in_b, int32_t epi, const uint16_t *res, const float *res_stats,
+                                      const float *res_g, const float *res_b, const float *g_next, uint16_t *out,
+                                      float *st_out, int32_t cfg)
+{
+    using namespace emb;
+    if (!fmt_valid(fmt) || K % 64 || N % 32 || M <= 0 || epi < 0 || epi > 2 || hip_device_count() == 0) return -1;
+    if ((in_stats && (!in_g || !in_b || epi == EPI_BIAS_RES)) || (epi == EPI_BIAS_RES && !res) ||
+        (res_stats && (!res_g || !res_b)) || (g_next && epi != EPI_BIAS_RES))
+        return -1;
     const int Mp = (int)align_up((size_t)M, GEMM_BM);
-    const size_t osz = 2;   // f16 out for every epilogue
-    char *dq = nullptr, *dd_ = nullptr, *dm = nullptr, *dx = nullptr, *db = nullptr, *dr = nullptr, *dout = nullptr;
-    HIP_RC(hipSetDevice(0));
-    HIP_RC(hipMalloc((void **)&dq, q.bytes.size()));
-    HIP_RC(hipMemcpy(dq, q.bytes.data(), q.bytes.size(), hipMemcpyHostToDevice));
-    if (!dd.bytes.empty()) {
-        HIP_RC(hipMalloc((void **)&dd_, dd.bytes.size()));
-        HIP_RC(hipMemcpy(dd_, dd.bytes.data(), dd.bytes.size(), hipMemcpyHostToDevice));
-    }
-    if (!mm.bytes.empty()) {
-        HIP_RC(hipMalloc((void **)&dm, mm.bytes.size()));
-        HIP_RC(hipMemcpy(dm, mm.bytes.data(), mm.bytes.size(), hipMemcpyHostToDevice));
-    }
-    HIP_RC(hipMalloc((void **)&dx, (size_t)Mp * K * 2));
-    HIP_RC(hipMemset(dx, 0, (size_t)Mp * K * 2));
-    HIP_RC(hipMemcpy(dx, x, (size_t)M * K * 2, hipMemcpyHostToDevice));
-    HIP_RC(hipMalloc((void **)&db, (size_t)N * 4));
-    HIP_RC(hipMemcpy(db, bias, (size_t)N * 4, hipMemcpyHostToDevice));
-    HIP_RC(hipMalloc((void **)&dout, (size_t)Mp * N * osz));
-    if (epi == EPI_BIAS_RES) {   // residual: f16 [M][N]
-        HIP_RC(hipMalloc((void **)&dr, (size_t)Mp * N * 2));
-        HIP_RC(hipMemset(dr, 0, (size_t)Mp * N * 2));
-        HIP_RC(hipMemcpy(dr, res, (size_t)M * N * 2, hipMemcpyHostToDevice));
-    }
+    DeviceGuard guard(0);
+    HIP_RC(guard.status());
+    HookBufs B;
+    HostTensor t;
     DevWeight W;
-    W.fmt = fdev; W.N = n_out; W.K = k_out;
-    W.qs = dq; W.d = (const uint16_t *)dd_; W.m = (const uint16_t *)dm; W.layout = layout;
-    g_force_bn = layout == 0 ? tile_n : 0;
-    g_gemm16_cfg = layout == 1 ? (tile_n & 0xff) : 0;
-    launch_gemm(W, (const uint16_t *)dx, Mp, (const float *)db, epi, (const void *)dr, dout, nullptr);
-    g_force_bn = 0;
-    g_gemm16_cfg = 0;
+    if (!hook_weight(fmt, N, K, w_rows, t, W, B)) return -1;
+    LnFold ln;
+    const float *dbias = (const float *)B.up(bias, (size_t)N * 4, 0);
+    if (in_stats) {
+        // the LN fold of the input: c1 = W gamma, c2 = bias + W beta
+        const HostTensor hb = vec_tensor(bias, N), hg = vec_tensor(in_g, K), hbt = vec_tensor(in_b, K);
+        Piece c1, c2;
+        fold_ln({&t}, {&hb}, hg, hbt, c1, c2);
+        ln.in_stats = (const float2 *)B.up(in_stats, (size_t)M * 8, (size_t)Mp * 8);
+        ln.c1 = (const float *)B.up(c1.bytes.data(), c1.bytes.size(), 0);
+        dbias = (const float *)B.up(c2.bytes.data(), c2.bytes.size(), 0);
+    }
+    void *dx = B.up(x, (size_t)M * K * 2, (size_t)Mp * K * 2);
+    void *dout = B.up(nullptr, 0, (size_t)Mp * N * 2);
+    float2 *dst = nullptr;
+    if (epi == EPI_BIAS_RES) {
+        B.up(nullptr, 0, 0);
+        void *dr = B.up(res, (size_t)M * N * 2, (size_t)Mp * N * 2);
+        dout = dr;   // in place, as the forward runs it
+        if (res_stats) {
+            ln.res_stats = (const float2 *)B.up(res_stats, (size_t)M * 8, (size_t)Mp * 8);
+            ln.res_g = (const float *)B.up(res_g, (size_t)N * 4, 0);
+            ln.res_b = (const float *)B.up(res_b, (size_t)N * 4, 0);
+        }
+        if (g_next) {
+            ln.g_next = (const float *)B.up(g_next, (size_t)N * 4, 0);
+            ln.part = (float2 *)B.up(nullptr, 0, (size_t)Mp * (N / 32) * 8);
+            ln.part_stride = Mp;
+            dst = (float2 *)B.up(nullptr, 0, (size_t)Mp * 8);
+        }
+    }
+    if (B.bad) return -1;
+    g_gemm_cfg = cfg;
+    const int rc = launch_gemm(W, (const uint16_t *)dx, Mp, dbias, epi, dout, dout, nullptr, ln);
+    g_gemm_cfg = 0;
+    if (rc != 0) return rc;
+    if (dst) launch_ln_stats(ln.part, N / 32, Mp, Mp, N, dst, nullptr);
     HIP_RC(hipGetLastError());
     HIP_RC(hipDeviceSynchronize());
-    HIP_RC(hipMemcpy(out, dout, (size_t)M * N * osz, hipMemcpyDeviceToHost));
-    for (char *p : {dq, dd_, dm, dx, db, dr, dout}) if (p) (void)hipFree(p);
+    HIP_RC(hipMemcpy(out, dout, (size_t)M * N * 2, hipMemcpyDeviceToHost));
+    if (dst && st_out) HIP_RC(hipMemcpy(st_out, dst, (size_t)M * 8, hipMemcpyDeviceToHost));
     return 0;
 }
 
 // ---------------------------------------------------------------------------
-// residual GEMM + the LayerNorm after it (bert_hip.h): fused panel form or the
-// separate LN kernel, device 0, host buffers
+// GEMM micro-benchmark (bert_hip.h): device-timed launches on random operands,
+// in the forward's own forms (LN fold on the input of epi 0/1; residual with
+// its LN, the next gamma and the partial statistics for epi 2)
 // ---------------------------------------------------------------------------
-extern "C" int32_t bertx_test_gemm_ln(int32_t fmt, int32_t N, int32_t K, const void *w_rows, const float *bias,
-                                      int32_t M, int32_t rows, const uint16_t *x, const uint16_t *res,
-                                      const float *stats, const float *lnw, const float *lnb, const float *nw,
-                                      const float *nb, uint16_t *out, uint16_t *xh, float *st_out, int32_t panel)
+extern "C" int32_t bertx_bench_gemm(int32_t fmt, int32_t N, int32_t K, int32_t M, int32_t epi, int32_t cfg,
+                                    int32_t iters, float *avg_us)
 {
     using namespace emb;
-    if (!fmt_valid(fmt) || K % 64 || N % 32 || M <= 0 || rows < 0 || rows > M || hip_device_count() == 0) return -1;
-    HostTensor t;
-    t.fmt = fmt; t.ne0 = K; t.ne1 = N;
-    t.bytes.assign((const uint8_t *)w_rows, (const uint8_t *)w_rows + fmt_row_bytes(fmt, K) * (size_t)N);
-    const int fdev = (fmt == FMT_F32 || fmt == FMT_F16) ? FMT_F16 : fmt;
-    Piece q, dd, mm;
-    int n_out = 0, k_out = 0;
-    repack_linear({&t}, fdev, q, dd, mm, n_out, k_out, 1);
+    if (!fmt_valid(fmt) || K % 64 || N % 32 || M <= 0 || iters <= 0 || epi < 0 || epi > 2 ||
+        hip_device_count() == 0)
+        return -1;
     const int Mp = (int)align_up((size_t)M, GEMM_BM);
-    std::vector<char *> bufs;
-    auto up = [&](const void *h, size_t bytes, size_t alloc) -> char * {
-        char *p = nullptr;
-        if (hipMalloc((void **)&p, std::max<size_t>(alloc, 16)) != hipSuccess) return nullptr;
-        bufs.push_back(p);
-        (void)hipMemset(p, 0, std::max<size_t>(alloc, 16));
-        if (h && bytes) (void)hipMemcpy(p, h, bytes, hipMemcpyHostToDevice);
-        return p;
-    };
-    HIP_RC(hipSetDevice(0));
-    DevWeight W;
-    W.fmt = fdev; W.N = n_out; W.K = k_out; W.layout = 1;
-    W.qs = up(q.bytes.data(), q.bytes.size(), q.bytes.size());
-    W.d = (const uint16_t *)(dd.bytes.empty() ? nullptr : up(dd.bytes.data(), dd.bytes.size(), dd.bytes.size()));
-    W.m = (const uint16_t *)(mm.bytes.empty() ? nullptr : up(mm.bytes.data(), mm.bytes.size(), mm.bytes.size()));
-    char *dx = up(x, (size_t)M * K * 2, (size_t)Mp * K * 2);
-    char *db = up(bias, (size_t)N * 4, (size_t)N * 4);
-    char *dy = up(res, (size_t)M * N * 2, (size_t)Mp * N * 2);   // in place: res -> out
-    char *dst = up(stats, stats ? (size_t)M * 8 : 0, (size_t)Mp * 8);
-    char *dw = up(lnw, (size_t)N * 4, (size_t)N * 4), *dbb = up(lnb, (size_t)N * 4, (size_t)N * 4);
-    char *dnw = up(nw, (size_t)N * 4, (size_t)N * 4), *dnb = up(nb, (size_t)N * 4, (size_t)N * 4);
-    char *dxh = up(nullptr, 0, (size_t)Mp * N * 2);
-    char *dcnt = up(nullptr, 0, (size_t)(Mp / 128 + 1) * 4);
-    int rc = 0;
-    for (char *p : bufs) rc |= p == nullptr;
-    if (!rc) {
-        ResLN r;
-        if (stats) { r.stats = (const float2 *)dst; r.w = (const float *)dw; r.b = (const float *)dbb; }
-        if (panel) {
-            r.cnt = (uint32_t *)dcnt; r.xh = (uint16_t *)dxh; r.st_out = (float2 *)dst;
-            r.nw = (const float *)dnw; r.nb = (const float *)dnb; r.rows = rows;
-        }
-        const int fused = launch_gemm(W, (const uint16_t *)dx, Mp, (const float *)db, EPI_BIAS_RES, dy, dy, nullptr, r);
-        if (panel && !fused) rc = -2;   // this shape has no panel form
-        if (!fused)
-            launch_layernorm((const uint16_t *)dy, rows, N, (const float *)dnw, (const float *)dnb, (uint16_t *)dxh,
-                             (float2 *)dst, nullptr);
-        if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = -1;
-        if (rc == 0) {
-            (void)hipMemcpy(out, dy, (size_t)M * N * 2, hipMemcpyDeviceToHost);
-            (void)hipMemcpy(xh, dxh, (size_t)M * N * 2, hipMemcpyDeviceToHost);
-            (void)hipMemcpy(st_out, dst, (size_t)M * 8, hipMemcpyDeviceToHost);
-        }
-    } else {
-        rc = -1;
-    }
-    for (char *p : bufs) if (p) (void)hipFree(p);
-    return rc;
-}
-
-// ---------------------------------------------------------------------------
-// GEMM micro-benchmark (bert_hip.h): device-timed launches on random operands
-// ---------------------------------------------------------------------------
-extern "C" int32_t bertx_bench_gemm(int32_t fmt, int32_t N, int32_t K, int32_t M, int32_t epi, int32_t tile_n,
-                                    int32_t ablate, int32_t iters, float *avg_us)
-{
-    using namespace emb;
-    if (K % 64 || N % 64 || M <= 0 || iters <= 0 || hip_device_count() == 0) return -1;
-    const int fdev = (fmt == FMT_F32 || fmt == FMT_F16) ? FMT_F16 : fmt;
-    const int Mp = (int)align_up((size_t)M, GEMM_BM);
-    const size_t nel = (size_t)N * K;
-    const size_t qbytes = fdev == FMT_F16 ? nel * 2 : (fdev == FMT_Q8_0 ? nel : nel / 2);
-    std::vector<uint8_t> hq(qbytes);
-    std::vector<uint16_t> hd(nel / 32), hx((size_t)Mp * K);
     uint32_t st = 12345u;
-    auto rnd = [&]() { st = st * 1664525u + 1013904223u; return st; };
-    for (auto &b : hq) b = (uint8_t)(rnd() >> 24);
-    if (fdev == FMT_F16)
-        for (size_t i = 0; i < nel; ++i) ((uint16_t *)hq.data())[i] = f32_to_f16(((rnd() >> 8) / 16777216.0f - 0.5f) * 0.1f);
-    for (auto &v : hd) v = f32_to_f16(0.001f + (rnd() >> 8) / 16777216.0f * 0.01f);
-    for (auto &v : hx) v = f32_to_f16((rnd() >> 8) / 16777216.0f - 0.5f);
-    char *dq = nullptr, *dd = nullptr, *dx = nullptr, *db = nullptr, *dr = nullptr, *dout = nullptr;
-    HIP_RC(hipSetDevice(0));
-    HIP_RC(hipMalloc((void **)&dq, qbytes));
-    HIP_RC(hipMemcpy(dq, hq.data(), qbytes, hipMemcpyHostToDevice));
-    HIP_RC(hipMalloc((void **)&dd, hd.size() * 2));
-    HIP_RC(hipMemcpy(dd, hd.data(), hd.size() * 2, hipMemcpyHostToDevice));
-    HIP_RC(hipMalloc((void **)&dx, hx.size() * 2));
-    HIP_RC(hipMemcpy(dx, hx.data(), hx.size() * 2, hipMemcpyHostToDevice));
-    HIP_RC(hipMalloc((void **)&db, (size_t)N * 4));
-    HIP_RC(hipMemset(db, 0, (size_t)N * 4));
-    HIP_RC(hipMalloc((void **)&dr, (size_t)Mp * N * 4));
-    HIP_RC(hipMemset(dr, 0, (size_t)Mp * N * 4));
-    HIP_RC(hipMalloc((void **)&dout, (size_t)Mp * N * 4));
-    // the residual form as the forward runs it: LN of the residual recomputed from
-    // per-row (mean, 1/sigma) and gamma/beta (kernels.h ResLN)
-    char *dst_ln = nullptr, *dwb = nullptr;
-    ResLN rln;
-    if (epi == EPI_BIAS_RES) {
-        std::vector<float> hs((size_t)Mp * 2), hwb((size_t)N * 2);
-        for (size_t i = 0; i < hs.size(); i += 2) { hs[i] = 0.01f; hs[i + 1] = 1.0f + (rnd() >> 24) / 2560.0f; }
-        for (size_t i = 0; i < hwb.size(); ++i) hwb[i] = i < (size_t)N ? 1.0f : 0.0f;
-        HIP_RC(hipMalloc((void **)&dst_ln, hs.size() * 4));
-        HIP_RC(hipMemcpy(dst_ln, hs.data(), hs.size() * 4, hipMemcpyHostToDevice));
-        HIP_RC(hipMalloc((void **)&dwb, hwb.size() * 4));
-        HIP_RC(hipMemcpy(dwb, hwb.data(), hwb.size() * 4, hipMemcpyHostToDevice));
-        rln.stats = (const float2 *)dst_ln;
-        rln.w = (const float *)dwb;
-        rln.b = (const float *)dwb + N;
+    auto rnd = [&]() { st = st * 1664525u + 1013904223u; return (st >> 8) / 16777216.0f; };
+    // random weights in the file format, quantized by the native quantizer's rows
+    std::vector<float> wrow((size_t)K);
+    std::vector<uint8_t> rows(fmt_row_bytes(fmt, K) * (size_t)N);
+    for (int n = 0; n < N; ++n) {
+        for (auto &v : wrow) v = (rnd() - 0.5f) * 0.1f;
+        quantize_row(fmt, wrow.data(), rows.data() + fmt_row_bytes(fmt, K) * (size_t)n, K);
     }
+    std::vector<uint16_t> hx((size_t)Mp * K);
+    for (auto &v : hx) v = f32_to_f16(rnd() - 0.5f);
+    std::vector<float> hb((size_t)N), hg((size_t)std::max(N, K)), hbt((size_t)std::max(N, K)), hs((size_t)Mp * 2);
+    for (auto &v : hb) v = (rnd() - 0.5f) * 0.1f;
+    for (auto &v : hg) v = 1.0f + (rnd() - 0.5f) * 0.2f;
+    for (auto &v : hbt) v = (rnd() - 0.5f) * 0.1f;
+    for (size_t i = 0; i < hs.size(); i += 2) { hs[i] = 0.01f; hs[i + 1] = 1.0f + rnd() * 0.1f; }
+    DeviceGuard guard(0);
+    HIP_RC(guard.status());
+    HookBufs B;
+    HostTensor t;
     DevWeight W;
-    W.fmt = fdev; W.N = N; W.K = K;
-    W.qs = dq; W.d = (const uint16_t *)dd; W.m = (const uint16_t *)dd;
-    // tile_n 0x1000 | cfg: gemm16 (layout 1) with that config; otherwise gemm.hip (layout 0)
-    W.layout = (tile_n & 0x1000) ? 1 : 0;
-    std::function<void()> launch = [&]() {
-        g_force_bn = W.layout ? 0 : tile_n;
-        g_gemm16_cfg = W.layout ? (tile_n & 0xff) : 0;
-        g_gemm_variant = ablate == -2 ? 2 : 0;   // -2: gemmqw everywhere
-        launch_gemm(W, (const uint16_t *)dx, Mp, (const float *)db, epi, (const void *)dr, dout, nullptr, rln);
-        g_force_bn = 0;
-        g_gemm16_cfg = 0;
-        g_gemm_variant = 0;
+    if (!hook_weight(fmt, N, K, rows.data(), t, W, B)) return -1;
+    LnFold ln;
+    const float *dbias = (const float *)B.up(hb.data(), hb.size() * 4, 0);
+    void *dx = B.up(hx.data(), hx.size() * 2, 0);
+    void *dout = B.up(nullptr, 0, (size_t)Mp * N * 2);
+    if (epi == EPI_BIAS_RES) {
+        ln.res_stats = (const float2 *)B.up(hs.data(), hs.size() * 4, 0);
+        ln.res_g = (const float *)B.up(hg.data(), (size_t)N * 4, 0);
+        ln.res_b = (const float *)B.up(hbt.data(), (size_t)N * 4, 0);
+        ln.g_next = ln.res_g;
+        ln.part = (float2 *)B.up(nullptr, 0, (size_t)Mp * (N / 32) * 8);
+        ln.part_stride = Mp;
+    } else {
+        ln.in_stats = (const float2 *)B.up(hs.data(), hs.size() * 4, 0);
+        ln.c1 = (const float *)B.up(hg.data(), (size_t)N * 4, 0);
+    }
+    if (B.bad) return -1;
+    auto launch = [&]() {
+        g_gemm_cfg = cfg;
+        launch_gemm(W, (const uint16_t *)dx, Mp, dbias, epi, dout, dout, nullptr, ln);
+        g_gemm_cfg = 0;
     };
-    if (ablate <= -3 && ablate >= -300 && fdev == FMT_Q4_0) {
-        // -3: stamps; -3 - d: stamps + ablation d of gemmqw (kernels.h)
-        const int diag = -3 - ablate;
-        // stamped diagnostics: one launch, per-wave phase cycles to stderr
-        // tile_n: 256 -> gemmqw 1 x 8, 128 -> gemmqw 2 x 4, 4 -> gemmqv BM 256, 5 -> gemmqv BM 128
-        // tile_n 0x1000 | c: gemm16 config c (1-3) with stamps
-        const int z16 = (tile_n & 0x1000) ? (tile_n & 0xff) : 0;
-        const int wm = tile_n == 128 ? 2 : tile_n == 4 ? 4 : tile_n == 5 ? 5 : 1;
-        const int nt = z16 == 1 ? (Mp / 256) * ((N + 255) / 256)
-                     : z16 == 2 ? (Mp / 256) * ((N + 127) / 128) / 2
-                     : z16 == 3 ? (Mp / 128) * ((N + 127) / 128) / 2
-                     : wm >= 4 ? (Mp / 128) * ((N + 127) / 128) * 4 / 8 : (Mp / GEMM_BM) * ((N + 256 / wm - 1) / (256 / wm));
-        // per wave: 4 s_memtime phase stamps (gemmqw: + realtime start/end and the CU id)
-        const int SW = wm == 1 ? 8 : 4;
-        uint64_t *dst = nullptr;
-        HIP_RC(hipMalloc((void **)&dst, (size_t)nt * 8 * SW * 8));
-        HIP_RC(hipMemset(dst, 0, (size_t)nt * 8 * SW * 8));
-        // 3 + iters stamped launches; the events time the last iters, the stamps are the last one's
-        hipEvent_t e0, e1;
-        HIP_RC(hipEventCreate(&e0));
-        HIP_RC(hipEventCreate(&e1));
-        for (int i = 0; i < 3 + iters; ++i) {
-            if (i == 3) HIP_RC(hipEventRecord(e0, nullptr));
-            if (z16) {
-                if (W.layout != 1) break;
-                launch_gemm16_stamped(W, (const uint16_t *)dx, Mp, (const float *)db, epi, (const void *)dr, dout,
-                                      nullptr, z16, dst);
-            } else {
-                launch_gemm_q_stamped(W, (const uint16_t *)dx, Mp, (const float *)db, epi, (const void *)dr, dout,
-                                      nullptr, wm, dst, diag);
-            }
-        }
-        HIP_RC(hipEventRecord(e1, nullptr));
-        HIP_RC(hipDeviceSynchronize());
-        float st_ms = 0.f;
-        HIP_RC(hipEventElapsedTime(&st_ms, e0, e1));
-        (void)hipEventDestroy(e0);
-        (void)hipEventDestroy(e1);
-        std::vector<uint64_t> h((size_t)nt * 8 * SW);
-        HIP_RC(hipMemcpy(h.data(), dst, h.size() * 8, hipMemcpyDeviceToHost));
-        (void)hipFree(dst);
-        std::vector<double> pro, loop, epi_c, wg;
-        uint64_t r0 = ~0ull, r1 = 0;
-        double busy = 0;                         // sum over tiles of (last wave end - first wave start), realtime
-        std::map<uint64_t, double> cu_busy;      // per CU
-        for (int b = 0; b < nt; ++b) {
-            uint64_t b0 = ~0ull, b1 = 0, cu = 0;
-            for (int w = 0; w < 8; ++w) {
-                const uint64_t *p = &h[((size_t)b * 8 + w) * SW];
-                if (!p[3]) continue;
-                pro.push_back((double)(p[1] - p[0]));
-                loop.push_back((double)(p[2] - p[1]) / (K / 64));
-                epi_c.push_back((double)(p[3] - p[2]));
-                wg.push_back((double)(p[3] - p[0]));
-                if (SW == 8 && p[5]) {
-                    b0 = std::min(b0, p[4]); b1 = std::max(b1, p[5]);
-                    cu = (p[6] >> 32) * 4096 + ((p[6] >> 8) & 0xfff);   // xcc, (se, sh, cu)
-                }
-            }
-            if (b1 > b0) {
-                r0 = std::min(r0, b0); r1 = std::max(r1, b1);
-                busy += (double)(b1 - b0);
-                cu_busy[cu] += (double)(b1 - b0);
-            }
-        }
-        auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v.empty() ? 0.0 : v[v.size() / 2]; };
-        std::fprintf(stderr, "stamps diag=%d N=%d K=%d M=%d wm=%d: tiles %d  median cycles: prologue %.0f  per-K-step %.0f  "
-                     "epilogue %.0f  wave total %.0f", diag, N, K, Mp, wm, nt, med(pro), med(loop), med(epi_c), med(wg));
-        if (r1 > r0) {
-            // s_memrealtime: 100 MHz
-            const double span_us = (double)(r1 - r0) / 100.0;
-            std::fprintf(stderr, "  | realtime span %.1f us, tile avg %.2f us, CUs used %zu, CU busy %.1f%%",
-                         span_us, busy / nt / 100.0, cu_busy.size(), 100.0 * busy / (double)(r1 - r0) / cu_busy.size());
-        }
-        std::fprintf(stderr, "  | stamped launches avg %.1f us\n", st_ms * 1000.0 / iters);
-    }
-    if (ablate <= -3 && ablate >= -300 && fdev == FMT_Q4_0 && (tile_n == 0 || tile_n == 256)) {
-        // time the diagnostic variant itself (same build without the stamps)
-        const int diag = -3 - ablate;
-        launch = [&, diag]() {
-            launch_gemm_q_stamped(W, (const uint16_t *)dx, Mp, (const float *)db, epi, (const void *)dr, dout,
-                                  nullptr, 1, nullptr, diag);
-        };
-    }
     for (int i = 0; i < 3; ++i) launch();
     hipEvent_t a, b;
     HIP_RC(hipEventCreate(&a));
@@ -930,7 +793,6 @@ extern "C" int32_t bertx_bench_gemm(int32_t fmt, int32_t N, int32_t K, int32_t M
     *avg_us = ms * 1000.0f / (float)iters;
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
-    for (char *p : {dq, dd, dx, db, dr, dout, dst_ln, dwb}) if (p) (void)hipFree(p);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -952,7 +814,8 @@ extern "C" int32_t bertx_bench_attention(int32_t n_seqs, int32_t len, int32_t n_
     for (int i = 0; i <= n_seqs; ++i) hcu[(size_t)i] = i * len;
     uint16_t *dq = nullptr, *dout = nullptr;
     int32_t *dcu = nullptr;
-    HIP_RC(hipSetDevice(0));
+    DeviceGuard guard(0);
+    HIP_RC(guard.status());
     HIP_RC(hipMalloc((void **)&dq, hq.size() * 2));
     HIP_RC(hipMemcpy(dq, hq.data(), hq.size() * 2, hipMemcpyHostToDevice));
     HIP_RC(hipMalloc((void **)&dcu, hcu.size() * 4));
@@ -992,7 +855,8 @@ extern "C" int32_t bertx_test_attention(const uint16_t *qkv, const int32_t *cu, 
     const size_t T = (size_t)cu[n_seqs];
     uint16_t *dq = nullptr, *dout = nullptr;
     int32_t *dcu = nullptr;
-    HIP_RC(hipSetDevice(0));
+    DeviceGuard guard(0);
+    HIP_RC(guard.status());
     HIP_RC(hipMalloc((void **)&dq, (T + 64) * 3 * d * 2));
     HIP_RC(hipMemset(dq, 0, (T + 64) * 3 * d * 2));
     HIP_RC(hipMemcpy(dq, qkv, T * 3 * d * 2, hipMemcpyHostToDevice));

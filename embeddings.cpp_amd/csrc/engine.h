@@ -16,7 +16,7 @@
 namespace emb {
 
 enum KClass : int32_t {
-    K_EMBED_LN = 0, K_GEMM_QKV, K_ATTENTION, K_GEMM_O, K_LAYERNORM, K_GEMM_FFN_UP, K_GEMM_FFN_DOWN, K_POOL_L2,
+    K_EMBED_LN = 0, K_GEMM_QKV, K_ATTENTION, K_GEMM_O, K_LN_STATS, K_GEMM_FFN_UP, K_GEMM_FFN_DOWN, K_POOL_L2,
     K_NUM_CLASSES
 };
 const char *kclass_name(int k);
@@ -29,7 +29,11 @@ struct KStats {
 
 struct DevLayer {
     DevWeight qkv, o, up, down;
-    float *b_qkv = nullptr, *b_o = nullptr, *b_up = nullptr, *b_down = nullptr;
+    float *b_o = nullptr, *b_down = nullptr;
+    // LN fold (kernels.h) of the projections that read a LayerNorm'd stream:
+    // c1 = W gamma, c2 = b + W beta of the LN in front (QKV: the previous layer's
+    // output LN or the embedding LN; FFN-up: this layer's attention-output LN)
+    float *c1_qkv = nullptr, *c2_qkv = nullptr, *c1_up = nullptr, *c2_up = nullptr;
     float *ln1_w = nullptr, *ln1_b = nullptr, *ln2_w = nullptr, *ln2_b = nullptr;
 };
 
@@ -75,8 +79,10 @@ public:
     // stream other than the previous forward's first waits (on the device) for
     // that forward's completion event, so calls on different streams never
     // overlap in the workspace.
+    // len2_sum: sum of the squared sentence lengths when the caller knows them
+    // (attention FLOP of the per-kernel stats), else -1.
     int forward(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, int max_len, int total_tokens, float *d_out,
-                hipStream_t s);
+                hipStream_t s, double len2_sum = -1.0);
 
     // Host-driven forward: packs tokens, H2D, forward, D2H, synchronous.
     // tokens[i] has lens[i] ids; out[i] receives n_embd floats.
@@ -129,7 +135,6 @@ private:
     float *ln_e_w_ = nullptr, *ln_e_b_ = nullptr;
     std::vector<DevLayer> layers_;
     int wfmt_ = FMT_F16;
-    int layout_ = 1;                // DevWeight::layout of the linear weights
 
     // workspace
     int64_t cap_tokens_ = 0, cap_seqs_ = 0, cap_pool_ = 0;   // cap_pool_: pool partial rows (seqs x chunks)
@@ -137,13 +142,14 @@ private:
     hipStream_t last_stream_ = nullptr;     // ... and the stream it ran on
     bool any_forward_ = false;
     char *ws_ = nullptr;
-    uint16_t *yh_ = nullptr;        // pre-LN residual stream (f16)
-    float2 *st_ = nullptr;          // (mean, 1/sigma) of its last LN
-    uint16_t *xh_ = nullptr, *qkv_ = nullptr, *att_ = nullptr, *ffn_ = nullptr;
+    uint16_t *z_ = nullptr;         // residual stream as z = y * gamma of its LN (f16, kernels.h)
+    float2 *st_ = nullptr;          // (mean, 1/sigma) of y
+    float2 *part_ = nullptr;        // [d/32][rows] group partials of the residual GEMMs
+    int64_t rows_ = 0;              // workspace rows (part_ stride)
+    uint16_t *qkv_ = nullptr, *att_ = nullptr, *ffn_ = nullptr;
     int32_t *d_ids_ = nullptr, *d_cu_ = nullptr;
     float *d_out_ = nullptr;
     float *pool_part_ = nullptr;
-    uint32_t *panel_cnt_ = nullptr; // per-128-row panel counters of the fused residual LN (ResLN::cnt)
     int32_t *h_ids_ = nullptr, *h_cu_ = nullptr;   // pinned staging
     float *h_out_ = nullptr;
 
@@ -151,12 +157,10 @@ private:
     std::vector<GraphEntry> graphs_;
     std::vector<GraphKey> seen_once_;   // a shape is captured on its second use
     bool use_graphs_ = true;
-    // BERT_PANEL_LN=1 at context creation: residual GEMMs also run the following
-    // LayerNorm (ResLN panel form; measured slower, so off by default)
-    bool panel_ln_ = [] { const char *e = std::getenv("BERT_PANEL_LN"); return e && *e == '1'; }();
 
     // profiling
     bool profiling_ = false;
+    double att_flop_ = 0.0;         // attention FLOP of the forward being launched
     std::vector<PendingEv> pending_;
     std::vector<hipEvent_t> free_events_;
     KStats stats_[K_NUM_CLASSES];

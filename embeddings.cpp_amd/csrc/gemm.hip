@@ -1,802 +1,415 @@
-// Linear layers for gfx950:  Y[m][n] = epi( sum_k X[m][k] * W[n][k] ),
-// X f16 [M][K] (tokens x features), W in f16 / q4_0 / q4_1 / q8_0 in the
-// "register" layout of kernels.h.  MFMA v_mfma_f32_32x32x16_f16 with A = W rows
-// (32 features) and B = X rows (32 tokens), so an accumulator lane is a token
-// and its registers hold runs of 4 consecutive features.
+// Linear layers on v_mfma_f32_16x16x32_f16 (gfx950), weights in the lane-order
+// layout of kernels.h (reference bert.cpp:994-1016, 1040-1045, 1059-1072).
 //
-// Weights never touch LDS.  Each lane loads exactly the bytes of its own A
-// fragments (one 16-B load per K-step for q4, two for q8, four for f16 -- the
-// repack makes them contiguous) into a 3-set register ring two K-steps ahead,
-// and expands quantized words to f16 in registers (nibble | 0x6400 magic, one
-// packed subtract and one packed multiply by the block scale) between MFMAs.
-// LDS carries only the activations, by LDS-DMA (global_load_lds_dwordx4) with
-// an XOR swizzle applied to the per-lane SOURCE address, so ds_read_b128 of a
-// B fragment is conflict-light.
+// Y[m][n] = epi( sum_k X[m][k] W[n][k] ).  A = 16 features x 32 k (one quant
+// block per feature, so each lane's scale is a single f16), B = 32 k x 16
+// tokens.  The 16x16x32 loop holds a higher clock under load than the 32x32x16
+// loop at the same cycles per FLOP (MI355X_MICROARCH.md, DVFS give-back item 7).
 //
-// Two kernels (both: waves along the FEATURES, so every A fragment feeds
-// 256/32 or 128/32 MFMAs and each weight byte is loaded by one wave):
-//   gemmqw: one 8-wave workgroup per CU, tile 256 tokens x 256 features
-//           (or 2 x 4 waves, 256 x 128), 3-stage X ring.
-//   gemmqv: two 4-wave workgroups per CU, tile BM (256 / 128) tokens x 128
-//           features, 2-stage X ring -- the co-resident workgroups drift apart
-//           so one's epilogue overlaps the other's MFMAs.
-// Waits: every K-step issues its loads, then an explicit `s_waitcnt vmcnt(N)`
-// equal to the operations known to be in flight -- a run-time no-op that tells
-// the compiler's waitcnt pass the current set has landed, so it adds no
-// vmcnt(0) (which would drain the LDS-DMA ring) before the MFMAs.  The K loop
-// runs whole unguarded triples (past the end the issues re-read step KS-1) so
-// that count is the same on every path the compiler sees.
-// Epilogue straight from the accumulators: bias, era GELU or residual add;
-// f16 rows widened to 16-B stores with v_permlane32_swap, f32 rows as 16-B runs.
+// Workgroup = NW waves, tile BM tokens x 32*NW features; wave w owns features
+// n0 + 32w .. +31 (two A fragments, a = 0/1 for +0 / +16) and all BM tokens
+// (NJ = BM/16 B fragments per k-slice, each feeding two MFMAs), so every
+// dequantized A fragment feeds NJ MFMA pairs and every weight byte is loaded by
+// exactly one wave.  Weights never touch LDS: each lane loads its own fragment
+// words (16 B q4, 32 B q8, 64 B f16 per K-step, plus 8 B of scales) into a 3-set
+// register ring two K-steps ahead and expands them between MFMAs.  X goes
+// through an NS-stage LDS ring by LDS-DMA (buffer_load ... lds) with the XOR
+// swizzle on the source address (chunk c ^ ((row>>1)&7)), which keeps the
+// B-operand row read (ds_read_b128, lanes = 16 rows x 4 chunks) conflict-free.
+//   NW 4, BM 256, NS 2 / BM 128, NS 4: two workgroups per CU (64 KiB each), so
+//   one's epilogue overlaps the other's MFMAs.
+// Epilogue: accumulator pairs of adjacent 16-token groups are exchanged with
+// v_permlane16_swap so each lane owns 8 consecutive features of one token
+// (16-B loads of bias / residual / LN parameters and one 16-B store); the
+// LayerNorm bookkeeping of kernels.h LnFold runs there.
 #include "device_common.h"
 #include "host_common.h"
 #include "kernels.h"
+#include "zregs.h"
 
-#include <type_traits>
+#include <cstdio>
+#include <cstdlib>
+#include <utility>
 
 namespace emb {
 
 namespace {
 
-constexpr int GM = GEMM_BM;   // 256 tokens per tile
-constexpr int GK = 64;
-constexpr int XS = 3;                        // X stages
-constexpr int X_BYTES = GM * GK * 2;          // 32 KiB
-
-
-// Weight words are ordinary (compiler-visible) loads: the compiler must own the
-// registers of an in-flight load (an asm load's destination can be reused by
-// the register allocator before the data arrives).  They are issued before the
-// step's LDS-DMA, so the compiler's wait at their first use (next step) only
-// retires X(ks+2), which has had a whole step of MFMAs to land.
-__device__ __forceinline__ uint4 gload16(const void *p) { return *(const uint4 *)p; }
-__device__ __forceinline__ uint32_t gload4(const void *p) { return *(const uint32_t *)p; }
-// pin: an empty volatile asm that "rewrites" the registers, so their uses
-// cannot be scheduled above the (side-effecting) explicit wait before it.
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void pin(uint4 &q)
+__device__ __forceinline__ uint32_t lds_u32(const void *p)
 {
-    u32x4 v = __builtin_bit_cast(u32x4, q);
-    asm volatile("" : "+v"(v));
-    q = __builtin_bit_cast(uint4, v);
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char *)p;
 }
-__device__ __forceinline__ void pin(uint32_t &v) { asm volatile("" : "+v"(v)); }
 
-template <int FMT>
-struct QRegs;   // one K-step of this lane's weight words for one 32-feature subtile
-
-template <int FMT>
-struct QRegsQ4 {
-    uint4 q;           // words kk = 0..3 of lane half h
-    uint32_t d, m;     // scale (and min) dword: (block 0, block 1)
-    static constexpr int LOADS = FMT == FMT_Q4_1 ? 3 : 2;
-    __device__ void load(const uint8_t *pq, const uint32_t *pd, const uint32_t *pm)
-    {
-        q = gload16(pq);
-        d = gload4(pd);
-        if (FMT == FMT_Q4_1) m = gload4(pm);
-    }
-    __device__ void pin_all() { pin(q); pin(d); if (FMT == FMT_Q4_1) pin(m); }
-    // A fragment of k-slice kk: 8 f16 = (q - 8) d  |  q d + m
-    __device__ h16x8 frag(int kk) const
-    {
-        const uint32_t w = kk == 0 ? q.x : kk == 1 ? q.y : kk == 2 ? q.z : q.w;
-        const uint16_t dh = kk < 2 ? (uint16_t)(d & 0xffffu) : (uint16_t)(d >> 16);
-        const h16x2 d2 = {as_h(dh), as_h(dh)};
-        h16x2 m2 = {(h16)0.0f, (h16)0.0f};
-        if (FMT == FMT_Q4_1) {
-            const uint16_t mh = kk < 2 ? (uint16_t)(m & 0xffffu) : (uint16_t)(m >> 16);
-            m2 = h16x2{as_h(mh), as_h(mh)};
-        }
-        const h16 o = FMT == FMT_Q4_1 ? (h16)-1024.0f : (h16)-1032.0f;
-        const h16x2 off = {o, o};
-        h16x8 a;
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            h16x2 hh = as_h2(and_or_vs(w >> (4 * p), 0x000F000Fu, 0x64006400u)) + off;
-            hh = FMT == FMT_Q4_1 ? hh * d2 + m2 : hh * d2;
-            a[2 * p] = hh[0];
-            a[2 * p + 1] = hh[1];
-        }
-        return a;
-    }
-};
-template <> struct QRegs<FMT_Q4_0> : QRegsQ4<FMT_Q4_0> {};
-template <> struct QRegs<FMT_Q4_1> : QRegsQ4<FMT_Q4_1> {};
-
-template <>
-struct QRegs<FMT_Q8_0> {
-    uint4 q0, q1;      // 8 bytes per k-slice: kk 0,1 in q0, kk 2,3 in q1
-    uint32_t d;
-    static constexpr int LOADS = 3;
-    __device__ void load(const uint8_t *pq, const uint32_t *pd, const uint32_t *)
-    {
-        q0 = gload16(pq);
-        q1 = gload16(pq + 16);
-        d = gload4(pd);
-    }
-    __device__ void pin_all() { pin(q0); pin(q1); pin(d); }
-    __device__ h16x8 frag(int kk) const
-    {
-        const uint32_t w0 = kk == 0 ? q0.x : kk == 1 ? q0.z : kk == 2 ? q1.x : q1.z;
-        const uint32_t w1 = kk == 0 ? q0.y : kk == 1 ? q0.w : kk == 2 ? q1.y : q1.w;
-        const uint16_t dh = kk < 2 ? (uint16_t)(d & 0xffffu) : (uint16_t)(d >> 16);
-        const h16x2 d2 = {as_h(dh), as_h(dh)};
-        const h16x2 off = {(h16)-1152.0f, (h16)-1152.0f};   // bytes (q ^ 0x80), order e0 e2 e1 e3
-        h16x8 a;
-        const h16x2 p0 = (as_h2((w0 & 0x00FF00FFu) | 0x64006400u) + off) * d2;
-        const h16x2 p1 = (as_h2(((w0 >> 8) & 0x00FF00FFu) | 0x64006400u) + off) * d2;
-        const h16x2 p2 = (as_h2((w1 & 0x00FF00FFu) | 0x64006400u) + off) * d2;
-        const h16x2 p3 = (as_h2(((w1 >> 8) & 0x00FF00FFu) | 0x64006400u) + off) * d2;
-        a[0] = p0[0]; a[1] = p0[1]; a[2] = p1[0]; a[3] = p1[1];
-        a[4] = p2[0]; a[5] = p2[1]; a[6] = p3[0]; a[7] = p3[1];
-        return a;
-    }
-};
-
-template <>
-struct QRegs<FMT_F16> {        // f16 weights (f32 files are converted at load): no expansion
-    uint4 q[4];                // k-slices kk = 0..3 of lane half h: 8 f16 each
-    static constexpr int LOADS = 4;
-    __device__ void load(const uint8_t *pq, const uint32_t *, const uint32_t *)
-    {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) q[i] = gload16(pq + 16 * i);
-    }
-    __device__ void pin_all()
-    {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) pin(q[i]);
-    }
-    __device__ h16x8 frag(int kk) const { return __builtin_bit_cast(h16x8, q[kk]); }
-};
-
-// weight bytes per (K-step, feature) record
-template <int FMT>
-constexpr int qrec_bytes() { return FMT == FMT_F16 ? 128 : FMT == FMT_Q8_0 ? 64 : 32; }
-
-// ---------------------------------------------------------------------------
-// gemmqw: the same contraction with the 8 waves laid out along the FEATURES.
-// Tile 256 tokens x BN features, BN = 32 * 8 / WM; wave w owns features
-// n0 + 32*(w % (8/WM)) .. +31 and tokens (w / (8/WM)) * 256/WM .. +256/WM-1.
-// Every A fragment (dequantized weights) therefore feeds 256/WM/32 MFMAs
-// (8 at WM = 1: half the dequant VALU per MFMA of the 2 x 4 layout) and each
-// weight byte is loaded by exactly one wave.  Weights: a 3-set register ring,
-// two K-steps ahead; X: 3-stage LDS-DMA ring, two K-steps ahead; one barrier
-// per K-step.  Epilogue straight from the accumulators (no LDS staging):
-// f16 rows widened to 16-B stores with v_permlane32_swap, f32 rows as 16-B
-// runs of 4 features.
-// ---------------------------------------------------------------------------
-// DIAG (diagnostics builds only): 0x10 stamps; ablations 0x1 no dequant (raw
-// words as A), 0x2 no B ds_reads (fragments from the prologue), 0x4 no barrier
-// in the K loop, 0x8 no MFMA.
-template <int FMT, int EPI, int WM, int DIAG = 0>
-__global__ __launch_bounds__(512, 1) void gemmqw_kernel(DevWeight W, const h16 *__restrict__ X,
-                                                        const float *__restrict__ bias, const void *__restrict__ res,
-                                                        void *__restrict__ out, int nN, int nTiles, ResLN rln,
-                                                        uint64_t *__restrict__ stamps = nullptr)
+// ds_read_b128 at base + OFF with the read's completion tracked by hand: the
+// asm keeps the issue order (hipcc's scheduler otherwise moves every read down
+// next to its MFMAs), zwait_lgkm ties the data to a counted s_waitcnt.
+template <int OFF>
+__device__ __forceinline__ h16x8 zds_read(uint32_t base)
 {
-    // STAMP (diagnostics build only): s_memtime at start / after the prologue /
-    // after the K loop / after the epilogue, per wave, into stamps[]
-    constexpr bool STAMP = (DIAG & 0x10) != 0;
-    uint64_t ts[4], rt0 = 0;
-    if constexpr (STAMP) { ts[0] = __builtin_amdgcn_s_memtime(); rt0 = __builtin_amdgcn_s_memrealtime(); }
-    constexpr int WN = 8 / WM;                 // waves along the features
-    constexpr int BN = 32 * WN;                // 256 (WM 1) or 128 (WM 2)
-    constexpr int TM = GM / WM;                // tokens per wave
-    constexpr int NJ = TM / 32;                // B fragments (32-token groups) per k-slice
-    constexpr int QB = qrec_bytes<FMT>();
-    constexpr int P = QRegs<FMT>::LOADS + 4;   // vector-memory ops issued per K-step per wave
-    __shared__ __attribute__((aligned(16))) char smem[XS * X_BYTES];
+    h16x8 r;
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(base), "i"(OFF));
+    return r;
+}
+template <int N>
+__device__ __forceinline__ void zwait_lgkm(h16x8 &r)
+{
+    asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(r) : "i"(N));
+}
 
+constexpr int ZPF = 4;   // B-fragment read-ahead in the K loop (items)
+
+// One K-step's MFMAs: B fragments (s, j) -> item i = s NJ + j, read ZPF items
+// ahead of their two MFMAs (a ring of ZPF + 1 fragments); A fragments
+// dequantized from the register set `cur` (s = 0 first half, s = 1 second).
+template <int NJ, class R, int... I>
+__device__ __forceinline__ void zmma_items(const R &cur, uint32_t b0, uint32_t b1, f32x4 (&acc)[2][NJ],
+                                           std::integer_sequence<int, I...>)
+{
+    constexpr int NI = 2 * NJ, PF = ZPF;
+    h16x8 bq[PF + 1];
+    auto rd = [&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        if constexpr (i < NI) bq[i % (PF + 1)] = zds_read<(i % NJ) << 11>(i < NJ ? b0 : b1);
+    };
+    auto pre = [&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        if constexpr (i < PF) rd(std::integral_constant<int, i>{});
+    };
+    (pre(std::integral_constant<int, I>{}), ...);
+    h16x8 a0 = cur.frag(0), a1 = cur.frag(2);
+    auto item = [&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        rd(std::integral_constant<int, i + PF>{});
+        constexpr int last = (i + PF < NI ? i + PF : NI - 1);
+        zwait_lgkm<last - i>(bq[i % (PF + 1)]);
+        if constexpr (i == NJ) { a0 = cur.frag(1); a1 = cur.frag(3); }
+        const h16x8 bf = bq[i % (PF + 1)];
+        acc[0][i % NJ] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, bf, acc[0][i % NJ], 0, 0, 0);
+        acc[1][i % NJ] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, bf, acc[1][i % NJ], 0, 0, 0);
+    };
+    (item(std::integral_constant<int, I>{}), ...);
+}
+
+// The tile body: workgroup b of a grid of nTiles tiles (nN column tiles),
+// staging X in `smem` (NS * BM * 128 B of LDS).
+template <int FMT, int EPI, int NW, int BM, int NS>
+__device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b, DevWeight W,
+                                           const h16 *__restrict__ X, const float *__restrict__ bias,
+                                           const void *__restrict__ res, void *__restrict__ out, int nN, int nTiles,
+                                           const LnFold &ln)
+{
+    constexpr int BN = 32 * NW;
+    constexpr int NJ = BM / 16;                 // 16-token B fragments per k-slice
+    constexpr int XB = BM * ZK * 2;             // bytes per X stage
+    constexpr int XG = XB / (64 * NW * 16);     // LDS-DMA instructions per wave per stage
+    constexpr int LQ = ZRegs<FMT>::LOADS;
+    constexpr int QB = ZRegs<FMT>::QB;
+    constexpr int P = LQ + XG;                  // vector-memory ops issued per K-step per wave
+    static_assert(NS >= 2 && NS <= 4 && XG >= 2 && XG % 2 == 0, "X ring");
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int b = blockIdx.x, xcd = b & 7, qq = nTiles >> 3, rr = nTiles & 7;
-    const int t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
-    const int m0 = (t / nN) * GM, n0 = (t % nN) * BN;
-    const int K = W.K, N = W.N, KS = K / GK;
-    const int wm = wave / WN, wn = wave % WN, lr = lane & 31, hi = lane >> 5;
-    const int nw = n0 + 32 * wn;               // this wave's first feature
-
-    const h16 *xp[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int r = 32 * wave + 8 * i + (lane >> 3);
-        xp[i] = X + (size_t)(m0 + r) * K + (((lane & 7) ^ ((r >> 1) & 7)) * 8);
-    }
-#define EMB_ISSUE_XW(ks_, stage_)                                                                   \
-    {                                                                                               \
-        char *dst_ = smem + (stage_) * X_BYTES + ((32 * wave) << 7);                                \
-        glds<16>(xp[0] + (ks_) * GK, dst_);                                                         \
-        glds<16>(xp[1] + (ks_) * GK, dst_ + (8 << 7));                                              \
-        glds<16>(xp[2] + (ks_) * GK, dst_ + (16 << 7));                                             \
-        glds<16>(xp[3] + (ks_) * GK, dst_ + (24 << 7));                                             \
-    }
-    const int nrow = min(nw + lr, N - 1);
-    const uint8_t *wq = (const uint8_t *)W.qs + (size_t)nrow * QB + (QB / 2) * hi;
-    const uint32_t *wd = (const uint32_t *)W.d + nrow;
-    const uint32_t *wmn = FMT == FMT_Q4_1 ? (const uint32_t *)W.m + nrow : nullptr;
-    const size_t qstep = (size_t)N * QB, sstep = (size_t)N;
-
-    f32x16 acc[NJ];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
-
-    // prologue: W(0), X(0), W(1), X(1) in flight; retire W(0), X(0)
-    QRegs<FMT> w0, w1, w2;
-    const int k1 = min(1, KS - 1);
-    w0.load(wq, wd, wmn);
-    EMB_ISSUE_XW(0, 0)
-    w1.load(wq + k1 * qstep, wd + k1 * sstep, FMT == FMT_Q4_1 ? wmn + k1 * sstep : nullptr);
-    EMB_ISSUE_XW(k1, 1)
-    wait_vmcnt<P>();
-    lds_barrier();
-    if constexpr (STAMP) ts[1] = __builtin_amdgcn_s_memtime();
-
-    const int sw = (lr >> 1) & 7;
-    const int rbase = (wm * TM + lr) << 7;
-    int st = 0;
-    if constexpr (DIAG & 0x80) {   // static priority for the younger half (waves 4-7)
-        if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
-    }
-    h16x8 bdiag[(DIAG & 0x2) ? NJ : 1];
-    if constexpr (DIAG & 0x2) {
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) bdiag[j] = *(const h16x8 *)(smem + rbase + (j << 12) + (hi << 4));
-    }
-
-// One K-step with CUR's weights: W(ks+2) -> NXT2, X(ks+2) -> its stage (clamped:
-// past the end the issues re-read step KS-1), explicit no-op wait declaring CUR
-// landed, MFMAs, then retire step ks+1's operands and barrier.
-#define EMB_WSTEP(CUR, NXT2, ks_)                                                                         \
-    {                                                                                                     \
-        const int ksx = (ks_);                                                                            \
-        const int st2 = st == 0 ? 2 : st - 1;                                                             \
-        {                                                                                                 \
-            const int k2 = min(ksx + 2, KS - 1);                                                          \
-            NXT2.load(wq + k2 * qstep, wd + k2 * sstep, FMT == FMT_Q4_1 ? wmn + k2 * sstep : nullptr);    \
-            EMB_ISSUE_XW(k2, st2)                                                                         \
-            wait_vmcnt<2 * P>();                                                                          \
-            CUR.pin_all();                                                                                \
-        }                                                                                                 \
-        const char *xs = smem + st * X_BYTES + rbase;                                                     \
-        if constexpr ((DIAG & 0x100) && NJ == 8) {                                                        \
-            /* B reads two ahead in a 3-register rotation, A of k-slice kk+1 expanded */                  \
-            /* during kk; sched_group_barrier pins [DS read, 2 VALU, MFMA] per slot */                    \
-            h16x8 bq[3];                                                                                  \
-            bq[0] = *(const h16x8 *)(xs + (0 << 12) + ((hi ^ sw) << 4));                                  \
-            bq[1] = *(const h16x8 *)(xs + (1 << 12) + ((hi ^ sw) << 4));                                  \
-            h16x8 a = CUR.frag(0), an = a;                                                                \
-            _Pragma("unroll") for (int idx = 0; idx < 32; ++idx)                                          \
-            {                                                                                             \
-                const int kk = idx >> 3, j = idx & 7;                                                     \
-                if (idx + 2 < 32) {                                                                       \
-                    const int i2 = idx + 2;                                                               \
-                    bq[i2 % 3] = *(const h16x8 *)(xs + ((i2 & 7) << 12) + (((2 * (i2 >> 3) + hi) ^ sw) << 4)); \
-                }                                                                                         \
-                if (j == 0 && kk > 0) a = an;                                                             \
-                if (j == 1 && kk < 3) an = CUR.frag(kk + 1);                                              \
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bq[idx % 3], acc[j], 0, 0, 0);         \
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                        \
-                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);                                        \
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                        \
-            }                                                                                             \
-        } else if constexpr (DIAG & 0x20) {                                                               \
-            /* software-pipelined: B fragments and A dequant of k-slice kk+1 issued */                   \
-            /* between the MFMAs of kk (sched_group_barrier pins the interleave) */                       \
-            h16x8 bc[NJ], bnx[NJ];                                                                        \
-            _Pragma("unroll") for (int j = 0; j < NJ; ++j) bc[j] = *(const h16x8 *)(xs + (j << 12) + ((hi ^ sw) << 4)); \
-            h16x8 ac = CUR.frag(0), anx;                                                                  \
-            _Pragma("unroll") for (int kk = 0; kk < 4; ++kk)                                              \
-            {                                                                                             \
-                if (kk < 3) {                                                                             \
-                    const int cx = ((2 * kk + 2 + hi) ^ sw) << 4;                                         \
-                    _Pragma("unroll") for (int j = 0; j < NJ; ++j) bnx[j] = *(const h16x8 *)(xs + (j << 12) + cx); \
-                    anx = CUR.frag(kk + 1);                                                               \
-                }                                                                                         \
-                _Pragma("unroll") for (int j = 0; j < NJ; ++j) acc[j] =                                   \
-                    __builtin_amdgcn_mfma_f32_32x32x16_f16(ac, bc[j], acc[j], 0, 0, 0);                   \
-                if (kk < 3) {                                                                             \
-                    _Pragma("unroll") for (int j = 0; j < NJ; ++j) {                                      \
-                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                \
-                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                \
-                        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);                                \
-                    }                                                                                     \
-                    _Pragma("unroll") for (int j = 0; j < NJ; ++j) bc[j] = bnx[j];                        \
-                    ac = anx;                                                                             \
-                }                                                                                         \
-            }                                                                                             \
-        } else                                                                                            \
-        _Pragma("unroll") for (int kk = 0; kk < 4; ++kk)                                                  \
-        {                                                                                                 \
-            const int cx = ((2 * kk + hi) ^ sw) << 4;                                                     \
-            h16x8 bf[NJ];                                                                                 \
-            if constexpr (DIAG & 0x2) {                                                                   \
-                _Pragma("unroll") for (int j = 0; j < NJ; ++j) bf[j] = bdiag[j];                          \
-            } else {                                                                                      \
-                _Pragma("unroll") for (int j = 0; j < NJ; ++j) bf[j] = *(const h16x8 *)(xs + (j << 12) + cx); \
-            }                                                                                             \
-            h16x8 a;                                                                                      \
-            if constexpr ((DIAG & 0x1) && FMT != FMT_F16) a = __builtin_bit_cast(h16x8, CUR.q);                               \
-            else a = CUR.frag(kk);                                                                        \
-            if constexpr (DIAG & 0x8) {                                                                   \
-                _Pragma("unroll") for (int j = 0; j < NJ; ++j) asm volatile("" :: "v"(a), "v"(bf[j]));   \
-            } else {                                                                                      \
-                if constexpr (DIAG & 0x40) __builtin_amdgcn_s_setprio(1);                                 \
-                _Pragma("unroll") for (int j = 0; j < NJ; ++j) acc[j] =                                   \
-                    __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bf[j], acc[j], 0, 0, 0);                    \
-                if constexpr (DIAG & 0x40) __builtin_amdgcn_s_setprio(0);                                 \
-            }                                                                                             \
-        }                                                                                                 \
-        wait_vmcnt<P>(); /* step ks+1's W and X landed; step ks+2's may fly */                           \
-        if constexpr (DIAG & 0x4) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                     \
-        else lds_barrier();                                                                               \
-        st = st == 2 ? 0 : st + 1;                                                                        \
-    }
-
-    // whole triples in the loop (no guarded steps: a guard is a path on which
-    // the compiler's waitcnt model loses track and drains with vmcnt(0)), then
-    // the 0-2 remaining steps
-    int ks = 0;
-    for (; ks + 3 <= KS; ks += 3) {
-        EMB_WSTEP(w0, w2, ks)
-        EMB_WSTEP(w1, w0, ks + 1)
-        EMB_WSTEP(w2, w1, ks + 2)
-    }
-    if (ks < KS) {
-        EMB_WSTEP(w0, w2, ks)
-        if (ks + 1 < KS) EMB_WSTEP(w1, w0, ks + 1)
-    }
-#undef EMB_WSTEP
-#undef EMB_ISSUE_XW
-    wait_vmcnt<0>();   // the clamped tail re-reads still write LDS / registers
-    if constexpr (STAMP) ts[2] = __builtin_amdgcn_s_memtime();
-
-    // ---- epilogue: lane holds token 32j + lr, features nw + 8g + 4hi + e ----
-    if (nw >= N) return;                       // wave-uniform (N % 32 == 0)
-    const int mrow = m0 + wm * TM + lr;
-    f32x4 bb[4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) bb[g] = *(const f32x4 *)(bias + nw + 8 * g + 4 * hi);
-    if constexpr (EPI == EPI_BIAS_RES) {
-        f32x4 lw[4], lb[4];
-        if (rln.stats) {
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                lw[g] = *(const f32x4 *)(rln.w + nw + 8 * g + 4 * hi);
-                lb[g] = *(const f32x4 *)(rln.b + nw + 8 * g + 4 * hi);
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const size_t rowo = (size_t)(mrow + 32 * j) * N + nw + 4 * hi;
-            f32x4 rv[4];
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const h16x4 r4 = *(const h16x4 *)((const h16 *)res + rowo + 8 * g);
-                rv[g] = f32x4{(float)r4[0], (float)r4[1], (float)r4[2], (float)r4[3]};
-            }
-            if (rln.stats) {                   // residual = LN(pre-LN row), recomputed
-                const float2 st = rln.stats[mrow + 32 * j];
-#pragma unroll
-                for (int g = 0; g < 4; ++g)
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) rv[g][e] = ln_apply(rv[g][e], st.x, st.y, lw[g][e], lb[g][e]);
-            }
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                h16x4 o;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) o[e] = (h16)(rv[g][e] + (bb[g][e] + acc[j][4 * g + e]));
-                *(h16x4 *)((h16 *)out + rowo + 8 * g) = o;
-            }
-        }
-    } else {
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            uint32_t pk[4][2];                 // group g: 4 f16 of features 8g + 4hi + 0..3
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                float v[4];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = bb[g][e] + acc[j][4 * g + e];
-                if constexpr (EPI == EPI_BIAS_GELU_F16) {
-                    pk[g][0] = gelu2_era(v[0], v[1]);
-                    pk[g][1] = gelu2_era(v[2], v[3]);
-                } else {
-                    pk[g][0] = __builtin_bit_cast(uint32_t, h16x2{(h16)v[0], (h16)v[1]});
-                    pk[g][1] = __builtin_bit_cast(uint32_t, h16x2{(h16)v[2], (h16)v[3]});
-                }
-            }
-            // T21: half-exchange pairs (g, g+1) -> lanes 0-31 hold features 8g..8g+7,
-            // lanes 32-63 hold 8g+8..8g+15 of the same token
-            h16 *orow = (h16 *)out + (size_t)(mrow + 32 * j) * N + nw + 8 * hi;
-#pragma unroll
-            for (int g = 0; g < 4; g += 2) {
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const auto r2 = __builtin_amdgcn_permlane32_swap(pk[g][h], pk[g + 1][h], false, false);
-                    pk[g][h] = r2[0];
-                    pk[g + 1][h] = r2[1];
-                }
-                uint4 v;
-                v.x = pk[g][0]; v.y = pk[g][1]; v.z = pk[g + 1][0]; v.w = pk[g + 1][1];
-                *(uint4 *)(orow + 8 * g) = v;
-            }
-        }
-    }
-    if constexpr (STAMP) {
-        ts[3] = __builtin_amdgcn_s_memtime();
-        const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
-        // HW_ID (CU / SE / SIMD) and XCC_ID: which CU ran this tile
-        const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
-        const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);
-        if (lane == 0) {
-            uint64_t *o = stamps + ((size_t)blockIdx.x * 8 + wave) * 8;
-            for (int i = 0; i < 4; ++i) o[i] = ts[i];
-            o[4] = rt0; o[5] = rt1; o[6] = ((uint64_t)xcc << 32) | hw;
-        }
-    }
-}
-
-template <int FMT, int WM, int STAMP = 0>
-void dispatch_qw(const DevWeight &W, const h16 *x, int M, const float *bias, int epi, const void *res, void *out,
-                 hipStream_t s, const ResLN &rln, uint64_t *stamps = nullptr)
-{
-    constexpr int BN = 256 / WM;
-    const int nN = (W.N + BN - 1) / BN, nTiles = (M / GM) * nN;
-    if (epi == EPI_BIAS_F16)
-        gemmqw_kernel<FMT, EPI_BIAS_F16, WM, STAMP><<<nTiles, 512, 0, s>>>(W, x, bias, res, out, nN, nTiles, rln, stamps);
-    else if (epi == EPI_BIAS_GELU_F16)
-        gemmqw_kernel<FMT, EPI_BIAS_GELU_F16, WM, STAMP><<<nTiles, 512, 0, s>>>(W, x, bias, res, out, nN, nTiles, rln,
-                                                                              stamps);
-    else
-        gemmqw_kernel<FMT, EPI_BIAS_RES, WM, STAMP><<<nTiles, 512, 0, s>>>(W, x, bias, res, out, nN, nTiles, rln,
-                                                                             stamps);
-}
-
-// ---------------------------------------------------------------------------
-// gemmqv: TWO workgroups per CU.  4 waves (256 threads) per workgroup, tile
-// BM tokens x 128 features, wave w owns features n0 + 32w .. +31 and all BM
-// tokens (NJ = BM/32 B fragments per k-slice).  Two independent workgroups per
-// CU drift apart, so one's epilogue (HBM store burst, GELU VALU) and prologue
-// overlap the other's MFMA loop -- with one workgroup per CU every CU hit its
-// epilogue at the same moment (measured: 30-40 % of the tile time).
-// X: 2-stage LDS-DMA ring (64 KiB at BM 256), one K-step ahead; W: 3-set
-// register ring, two K-steps ahead; one barrier per K-step.
-// ---------------------------------------------------------------------------
-template <int FMT, int EPI, int BM, int NS, bool STAMP = false>
-__global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemmqv_kernel(DevWeight W, const h16 *__restrict__ X,
-                                                        const float *__restrict__ bias, const void *__restrict__ res,
-                                                        void *__restrict__ out, int nN, int nTiles, ResLN rln,
-                                                        uint64_t *__restrict__ stamps = nullptr)
-{
-    uint64_t ts[4];   // STAMP (diagnostics only): start / after prologue / after K loop / end
-    if constexpr (STAMP) ts[0] = __builtin_amdgcn_s_memtime();
-    constexpr int BN = 128;
-    constexpr int NJ = BM / 32;
-    constexpr int XB = BM * GK * 2;            // bytes per X stage
-    constexpr int XG = XB / (256 * 16);        // LDS-DMA instructions per wave per stage
-    constexpr int QB = qrec_bytes<FMT>();
-    constexpr int LQ = QRegs<FMT>::LOADS;
-    constexpr int P = LQ + XG;                  // ops issued per K-step per wave
-    static_assert(NS >= 2 && NS <= 4, "X ring depth");
-    __shared__ __attribute__((aligned(16))) char smem[NS * XB];
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int b = blockIdx.x, xcd = b & 7, qq = nTiles >> 3, rr = nTiles & 7;
+    // XCD-aware bijective remap: consecutive tiles (same token panel) land on one
+    // XCD's L2 (workgroups are dealt to the 8 XCDs round-robin)
+    const int xcd = b & 7, qq = nTiles >> 3, rr = nTiles & 7;
     const int t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
     const int m0 = (t / nN) * BM, n0 = (t % nN) * BN;
-    const int K = W.K, N = W.N, KS = K / GK;
-    const int lr = lane & 31, hi = lane >> 5;
-    const int nw = n0 + 32 * wave;
+    const int K = W.K, N = W.N, KS = K / ZK;
+    const int fr = lane & 15, g = lane >> 4;
+    const int nw = n0 + 32 * wave;              // this wave's first feature
+    const int grp = min(nw, N - 32) >> 5;       // its 32-feature weight group (clamped past N)
 
-    // X LDS-DMA sources: XG instructions per wave, rows (XG*8)*wave + 8i + lane/8
-    const h16 *xp[XG];
+    // LDS-DMA of X as buffer loads: the tile's BM rows are the buffer (reads
+    // past it give 0); instruction i of this wave fills rows 8*XG*wave + 8i +
+    // lane/8; the swizzle ((row>>1)&7) only differs between even and odd i, so
+    // one offset VGPR per parity and the row step in soffset
+    const __amdgpu_buffer_rsrc_t xrs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(X + (size_t)m0 * K), (short)0, BM * K * 2, 0x00020000);
+    uint32_t xvo[2];
 #pragma unroll
-    for (int i = 0; i < XG; ++i) {
+    for (int i = 0; i < 2; ++i) {
         const int r = 8 * XG * wave + 8 * i + (lane >> 3);
-        xp[i] = X + (size_t)(m0 + r) * K + (((lane & 7) ^ ((r >> 1) & 7)) * 8);
+        xvo[i] = (uint32_t)(r * K + (((lane & 7) ^ ((r >> 1) & 7)) * 8)) * 2u;
     }
-#define EMB_ISSUE_XV(ks_, stage_)                                                                   \
-    {                                                                                               \
-        char *dst_ = smem + (stage_) * XB + ((8 * XG * wave) << 7);                                 \
-        _Pragma("unroll") for (int i = 0; i < XG; ++i) glds<16>(xp[i] + (ks_) * GK, dst_ + (i << 10)); \
-    }
-    const int nrow = min(nw + lr, N - 1);
-    const uint8_t *wq = (const uint8_t *)W.qs + (size_t)nrow * QB + (QB / 2) * hi;
-    const uint32_t *wd = (const uint32_t *)W.d + nrow;
-    const uint32_t *wmn = FMT == FMT_Q4_1 ? (const uint32_t *)W.m + nrow : nullptr;
-    const size_t qstep = (size_t)N * QB, sstep = (size_t)N;
-
-    f32x16 acc[NJ];
+    auto issue_x = [&](int ks, int stage) {
+        char *dst = smem + stage * XB + ((8 * XG * wave) << 7);
 #pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+        for (int i = 0; i < XG; ++i)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_void_t *)(dst + (i << 10)), 16, xvo[i & 1],
+                                                     ((i >> 1) * 16 * K + ks * ZK) * 2, 0, 0);
+    };
+    const uint8_t *wq = (const uint8_t *)W.qs + ((size_t)grp * 64 + lane) * QB;
+    const uint16_t *wd = W.d + ((size_t)grp * 16 + fr) * 4;
+    const uint16_t *wmn = FMT == FMT_Q4_1 ? W.m + ((size_t)grp * 16 + fr) * 4 : nullptr;
+    const size_t qstep = (size_t)N * 2 * QB, sstep = (size_t)N * 2;
+    auto wload = [&](ZRegs<FMT> &w, int ks) {
+        w.load(wq + ks * qstep, wd + ks * sstep, FMT == FMT_Q4_1 ? wmn + ks * sstep : nullptr);
+    };
 
-    // prologue: W(0), X(0) in flight first, then what the loop expects to be
-    // in flight at the end of step -1; retire W(0) and X(0)
-    QRegs<FMT> w0, w1, w2;
+    f32x4 acc[2][NJ];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[a][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    ZRegs<FMT> w0, w1, w2;
     const int k1 = min(1, KS - 1);
-    w0.load(wq, wd, wmn);
-    EMB_ISSUE_XV(0, 0)
-    if constexpr (NS == 2) {               // order X, W: W(1)
-        w1.load(wq + k1 * qstep, wd + k1 * sstep, FMT == FMT_Q4_1 ? wmn + k1 * sstep : nullptr);
+    wload(w0, 0);
+    issue_x(0, 0);
+    if constexpr (NS == 2) {
+        wload(w1, k1);
         wait_vmcnt<LQ>();
-    } else if constexpr (NS == 3) {        // order W, X: [W(1), X(1)]
+    } else if constexpr (NS == 3) {
         asm volatile("" ::: "memory");
-        w1.load(wq + k1 * qstep, wd + k1 * sstep, FMT == FMT_Q4_1 ? wmn + k1 * sstep : nullptr);
+        wload(w1, k1);
         asm volatile("" ::: "memory");
-        EMB_ISSUE_XV(k1, 1)
+        issue_x(k1, 1);
         wait_vmcnt<P>();
-    } else {                               // X(1), [W(1), X(2)]
-        EMB_ISSUE_XV(k1, 1)
+    } else {
+        issue_x(k1, 1);
         asm volatile("" ::: "memory");
-        w1.load(wq + k1 * qstep, wd + k1 * sstep, FMT == FMT_Q4_1 ? wmn + k1 * sstep : nullptr);
+        wload(w1, k1);
         asm volatile("" ::: "memory");
-        EMB_ISSUE_XV(min(2, KS - 1), 2)
+        issue_x(min(2, KS - 1), 2);
         wait_vmcnt<P + XG>();
     }
     lds_barrier();
 
-    if constexpr (STAMP) ts[1] = __builtin_amdgcn_s_memtime();
-    const int sw = (lr >> 1) & 7;
-    const int rbase = lr << 7;
+    const int sw = (fr >> 1) & 7;
+    const int rbase = fr << 7;
     int st = 0;
-
-// One K-step with CUR's weights: X(ks+1) -> the other stage, W(ks+2) -> NXT2
-// (clamped past the end), explicit no-op wait declaring CUR landed, MFMAs, then
-// retire X(ks+1) and W(ks+1) (everything but W(ks+2)) and barrier.
-#define EMB_VSTEP(CUR, NXT2, ks_)                                                                         \
-    {                                                                                                     \
-        const int ksx = (ks_);                                                                            \
-        {                                                                                                 \
-            const int kx = min(ksx + NS - 1, KS - 1), k2 = min(ksx + 2, KS - 1);                          \
-            const int sx = st == 0 ? NS - 1 : st - 1;   /* stage of X(ks + NS - 1) */                      \
-            if constexpr (NS == 2) {                                                                      \
-                EMB_ISSUE_XV(kx, sx)                                                                      \
-                asm volatile("" ::: "memory"); /* keep X(ks+1) older than W(ks+2): the end wait splits them */ \
-                NXT2.load(wq + k2 * qstep, wd + k2 * sstep, FMT == FMT_Q4_1 ? wmn + k2 * sstep : nullptr); \
-                wait_vmcnt<2 * LQ + XG>();                                                                \
-            } else {                                                                                      \
-                NXT2.load(wq + k2 * qstep, wd + k2 * sstep, FMT == FMT_Q4_1 ? wmn + k2 * sstep : nullptr); \
-                asm volatile("" ::: "memory"); /* W older than X: the end wait splits them */             \
-                EMB_ISSUE_XV(kx, sx)                                                                      \
-                wait_vmcnt<2 * P + (NS == 4 ? XG : 0)>();                                                 \
-            }                                                                                             \
-            CUR.pin_all();                                                                                \
-        }                                                                                                 \
-        const char *xs = smem + st * XB + rbase;                                                          \
-        if constexpr (NJ <= 4) {  /* B fragments double-buffered across k-slices */                       \
-            h16x8 bf[NJ], bn[NJ];                                                                         \
-            _Pragma("unroll") for (int j = 0; j < NJ; ++j) bf[j] = *(const h16x8 *)(xs + (j << 12) + (hi ^ sw) * 16); \
-            _Pragma("unroll") for (int kk = 0; kk < 4; ++kk)                                              \
-            {                                                                                             \
-                if (kk < 3) {                                                                             \
-                    const int cx = ((2 * kk + 2 + hi) ^ sw) << 4;                                         \
-                    _Pragma("unroll") for (int j = 0; j < NJ; ++j) bn[j] = *(const h16x8 *)(xs + (j << 12) + cx); \
-                }                                                                                         \
-                const h16x8 a = CUR.frag(kk);                                                             \
-                _Pragma("unroll") for (int j = 0; j < NJ; ++j) acc[j] =                                   \
-                    __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bf[j], acc[j], 0, 0, 0);                    \
-                if (kk < 3) {                                                                             \
-                    _Pragma("unroll") for (int j = 0; j < NJ; ++j) bf[j] = bn[j];                         \
-                }                                                                                         \
-            }                                                                                             \
-        } else {                  /* NJ = 8: registers are tight (acc alone is 128) */                     \
-            _Pragma("unroll") for (int kk = 0; kk < 4; ++kk)                                              \
-            {                                                                                             \
-                const int cx = ((2 * kk + hi) ^ sw) << 4;                                                 \
-                h16x8 bf[NJ];                                                                             \
-                _Pragma("unroll") for (int j = 0; j < NJ; ++j) bf[j] = *(const h16x8 *)(xs + (j << 12) + cx); \
-                const h16x8 a = CUR.frag(kk);                                                             \
-                _Pragma("unroll") for (int j = 0; j < NJ; ++j) acc[j] =                                   \
-                    __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bf[j], acc[j], 0, 0, 0);                    \
-            }                                                                                             \
-        }                                                                                                 \
-        /* X(ks+1), W(ks+1) landed; younger issues may fly */                                          \
-        if constexpr (NS == 2) wait_vmcnt<LQ>();                                                          \
-        else if constexpr (NS == 3) wait_vmcnt<P>();                                                      \
-        else wait_vmcnt<P + XG>();                                                                        \
-        lds_barrier();                                                                                    \
-        st = st == NS - 1 ? 0 : st + 1;                                                                   \
-    }
-
+    // One K-step with CUR's weights: issue X(ks + NS - 1) into the stage freed by
+    // the previous step and W(ks + 2) into the third register set, then an
+    // explicit vmcnt equal to what is provably still in flight (a run-time no-op
+    // that stops hipcc's waitcnt pass from draining the ring with vmcnt(0)); the
+    // K loop runs whole, unguarded triples so the count holds on every path.
+    auto kstep = [&](ZRegs<FMT> &cur, ZRegs<FMT> &nxt2, int ks) {
+        const int kx = min(ks + NS - 1, KS - 1), k2 = min(ks + 2, KS - 1);
+        const int sx = st == 0 ? NS - 1 : st - 1;
+        if constexpr (NS == 2) {
+            issue_x(kx, sx);
+            asm volatile("" ::: "memory");
+            wload(nxt2, k2);
+            wait_vmcnt<2 * LQ + XG>();
+        } else {
+            wload(nxt2, k2);
+            asm volatile("" ::: "memory");
+            issue_x(kx, sx);
+            wait_vmcnt<2 * P + (NS == 4 ? XG : 0)>();
+        }
+        cur.pin_all();
+        const uint32_t xs = lds_u32(smem + st * XB + rbase);
+        zmma_items<NJ>(cur, xs + ((g ^ sw) << 4), xs + (((4 + g) ^ sw) << 4), acc,
+                       std::make_integer_sequence<int, 2 * NJ>{});
+        if constexpr (NS == 2) wait_vmcnt<LQ>();
+        else if constexpr (NS == 3) wait_vmcnt<P>();
+        else wait_vmcnt<P + XG>();
+        lds_barrier();
+        st = st == NS - 1 ? 0 : st + 1;
+    };
     int ks = 0;
     for (; ks + 3 <= KS; ks += 3) {
-        EMB_VSTEP(w0, w2, ks)
-        EMB_VSTEP(w1, w0, ks + 1)
-        EMB_VSTEP(w2, w1, ks + 2)
+        kstep(w0, w2, ks);
+        kstep(w1, w0, ks + 1);
+        kstep(w2, w1, ks + 2);
     }
     if (ks < KS) {
-        EMB_VSTEP(w0, w2, ks)
-        if (ks + 1 < KS) EMB_VSTEP(w1, w0, ks + 1)
+        kstep(w0, w2, ks);
+        if (ks + 1 < KS) kstep(w1, w0, ks + 1);
     }
-#undef EMB_VSTEP
-#undef EMB_ISSUE_XV
     wait_vmcnt<0>();
-    if constexpr (STAMP) ts[2] = __builtin_amdgcn_s_memtime();
 
-    // ---- epilogue: lane holds token m0 + 32j + lr, features nw + 8g + 4hi + e ----
-    if (nw >= N) return;                       // wave-uniform (N % 32 == 0)
-    const int mrow = m0 + lr;
-    f32x4 bb[4];
+    // ---- epilogue ----
+    // acc[a][j] lane (g, fr): token m0 + 16j + fr, features nw + 16a + 4g + 0..3.
+    // After the permlane16 exchange of (acc[a][j], acc[a][j+1]) the lane holds
+    // token m0 + 16(j + (g&1)) + fr, features nw + 16a + 8(g>>1) + 0..7; lane
+    // l ^ 32 holds the other 16 of the wave's 32 features of the same token.
+    if (nw >= N) return;                        // wave-uniform (N % 32 == 0)
+    const int cb = nw + 8 * (g >> 1);           // feature of v[0][0]; v[1][*] at cb + 16
+    auto col8 = [&](const float *p, f32x4 (&o)[2][2]) {
 #pragma unroll
-    for (int g = 0; g < 4; ++g) bb[g] = *(const f32x4 *)(bias + nw + 8 * g + 4 * hi);
-    if constexpr (EPI == EPI_BIAS_RES) {
-        f32x4 rv[NJ][4];                       // all residual loads in flight at once
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const h16x4 r4 = *(const h16x4 *)((const h16 *)res + (size_t)(mrow + 32 * j) * N + nw + 4 * hi + 8 * g);
-                rv[j][g] = f32x4{(float)r4[0], (float)r4[1], (float)r4[2], (float)r4[3]};
-            }
-        if (rln.stats) {                       // residual = LN(pre-LN row), recomputed
-            f32x4 lw[4], lb[4];
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                lw[g] = *(const f32x4 *)(rln.w + nw + 8 * g + 4 * hi);
-                lb[g] = *(const f32x4 *)(rln.b + nw + 8 * g + 4 * hi);
-            }
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                const float2 st = rln.stats[mrow + 32 * j];
-#pragma unroll
-                for (int g = 0; g < 4; ++g)
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) rv[j][g][e] = ln_apply(rv[j][g][e], st.x, st.y, lw[g][e], lb[g][e]);
-            }
+        for (int a = 0; a < 2; ++a) {
+            o[a][0] = *(const f32x4 *)(p + cb + 16 * a);
+            o[a][1] = *(const f32x4 *)(p + cb + 16 * a + 4);
         }
+    };
+    f32x4 bb[2][2];
+    col8(bias, bb);
+    constexpr bool RES = EPI == EPI_BIAS_RES;
+    const bool lni = !RES && ln.in_stats;       // input LayerNorm folded (wave-uniform)
+    const bool rln = RES && ln.res_stats;       // residual given as z = y * gamma of an LN
+    const bool nxt = RES && ln.g_next;          // emit z' = y' * g_next and partial statistics
+    f32x4 c1[2][2], rg[2][2], gn[2][2];
+    if (lni) col8(ln.c1, c1);
+    if (rln) {
+        // the residual LN's beta joins the bias: v = acc + r z + (t gamma + (bias + beta))
+        f32x4 rb[2][2];
+        col8(ln.res_g, rg);
+        col8(ln.res_b, rb);
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const size_t rowo = (size_t)(mrow + 32 * j) * N + nw + 4 * hi;
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                h16x4 o;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) o[e] = (h16)(rv[j][g][e] + (bb[g][e] + acc[j][4 * g + e]));
-                *(h16x4 *)((h16 *)out + rowo + 8 * g) = o;
-            }
-        }
-    } else {
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            uint32_t pk[4][2];
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                float v[4];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = bb[g][e] + acc[j][4 * g + e];
-                if constexpr (EPI == EPI_BIAS_GELU_F16) {
-                    pk[g][0] = gelu2_era(v[0], v[1]);
-                    pk[g][1] = gelu2_era(v[2], v[3]);
-                } else {
-                    pk[g][0] = __builtin_bit_cast(uint32_t, h16x2{(h16)v[0], (h16)v[1]});
-                    pk[g][1] = __builtin_bit_cast(uint32_t, h16x2{(h16)v[2], (h16)v[3]});
-                }
-            }
-            h16 *orow = (h16 *)out + (size_t)(mrow + 32 * j) * N + nw + 8 * hi;
-#pragma unroll
-            for (int g = 0; g < 4; g += 2) {
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const auto r2 = __builtin_amdgcn_permlane32_swap(pk[g][h], pk[g + 1][h], false, false);
-                    pk[g][h] = r2[0];
-                    pk[g + 1][h] = r2[1];
-                }
-                uint4 v;
-                v.x = pk[g][0]; v.y = pk[g][1]; v.z = pk[g + 1][0]; v.w = pk[g + 1][1];
-                *(uint4 *)(orow + 8 * g) = v;
-            }
-        }
+        for (int a = 0; a < 2; ++a) { bb[a][0] += rb[a][0]; bb[a][1] += rb[a][1]; }
     }
-    if constexpr (STAMP) {
-        ts[3] = __builtin_amdgcn_s_memtime();
-        if (lane == 0)
-            for (int i = 0; i < 4; ++i) stamps[((size_t)blockIdx.x * 4 + wave) * 4 + i] = ts[i];
+    if (nxt) col8(ln.g_next, gn);
+    const float2 *stp = RES ? ln.res_stats : ln.in_stats;
+    const bool use_st = RES ? rln : lni;
+    // every residual row chunk and LN statistic of up to 8 token pairs in flight
+    // before the first use (one latency, not one per pair)
+    constexpr int JC = NJ < 16 ? NJ : 8;        // token groups per prefetch chunk
+#pragma unroll
+    for (int jc = 0; jc < NJ; jc += JC) {
+        uint4 rr[JC / 2][2];
+        float2 sts[JC / 2];
+#pragma unroll
+        for (int jp = 0; jp < JC / 2; ++jp) {
+            const int tok = m0 + 16 * (jc + 2 * jp + (g & 1)) + fr;
+            sts[jp] = use_st ? stp[tok] : float2{0.f, 1.f};
+            if constexpr (RES) {
+#pragma unroll
+                for (int a = 0; a < 2; ++a)
+                    rr[jp][a] = *(const uint4 *)((const h16 *)res + (size_t)tok * N + cb + 16 * a);
+            }
+        }
+#pragma unroll
+        for (int j = jc; j < jc + JC; j += 2) {
+            const int tok = m0 + 16 * (j + (g & 1)) + fr;
+            const float2 stt = sts[(j - jc) >> 1];
+            // (mean, 1/sigma) -> v = r x + t with t = -mean / sigma
+            const float sr = stt.y, st0 = -stt.x * stt.y;
+            float v[2][8];
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    v[a][e] = acc[a][j][e];
+                    v[a][4 + e] = acc[a][j + 1][e];
+                    zswap(v[a][e], v[a][4 + e]);
+                }
+            if constexpr (!RES) {
+#pragma unroll
+                for (int a = 0; a < 2; ++a)
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        const float bv = bb[a][e >> 2][e & 3];
+                        // input LN fold: LN(y) W^T + b = r (z W^T - mean c1) + c2
+                        v[a][e] = lni ? fmaf(sr, v[a][e], fmaf(st0, c1[a][e >> 2][e & 3], bv)) : v[a][e] + bv;
+                    }
+            } else {
+#pragma unroll
+                for (int a = 0; a < 2; ++a) {
+                    const h16x8 rh = __builtin_bit_cast(h16x8, rr[(j - jc) >> 1][a]);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        const float z = (float)rh[e], bv = bb[a][e >> 2][e & 3];
+                        // LN(y) = r z - r mean gamma + beta with z = y gamma (the stored stream)
+                        v[a][e] += rln ? fmaf(sr, z, fmaf(st0, rg[a][e >> 2][e & 3], bv)) : z + bv;
+                    }
+                }
+                if (nxt) {
+                    // this token's 32 features of the new stream y': sum and squared
+                    // deviations from their own mean (combined per row by ln_stats)
+                    float s = 0.f;
+#pragma unroll
+                    for (int a = 0; a < 2; ++a)
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) s += v[a][e];
+                    s = halves_sum(s);
+                    const float mg = s * (1.0f / 32.0f);
+                    float q = 0.f;
+#pragma unroll
+                    for (int a = 0; a < 2; ++a)
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) { const float u = v[a][e] - mg; q = fmaf(u, u, q); }
+                    q = halves_sum(q);
+                    if (g < 2) ln.part[(size_t)(nw >> 5) * ln.part_stride + tok] = float2{s, q};
+#pragma unroll
+                    for (int a = 0; a < 2; ++a)
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) v[a][e] *= gn[a][e >> 2][e & 3];
+                }
+            }
+#pragma unroll
+            for (int a = 0; a < 2; ++a) {
+                uint4 pk;
+                uint32_t *pw = (uint32_t *)&pk;
+                if constexpr (EPI == EPI_BIAS_GELU_F16) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) pw[e] = gelu2_era(v[a][2 * e], v[a][2 * e + 1]);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        pw[e] = __builtin_bit_cast(uint32_t, h16x2{(h16)v[a][2 * e], (h16)v[a][2 * e + 1]});
+                }
+                *(uint4 *)((h16 *)out + (size_t)tok * N + cb + 16 * a) = pk;
+            }
+        }
     }
 }
 
-template <int FMT, int BM>
-void dispatch_qv(const DevWeight &W, const h16 *x, int M, const float *bias, int epi, const void *res, void *out,
-                 hipStream_t s, const ResLN &rln)
+template <int FMT, int EPI, int NW, int BM, int NS>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void gemmz_kernel(DevWeight W, const h16 *__restrict__ X,
+                                                               const float *__restrict__ bias,
+                                                               const void *__restrict__ res, void *__restrict__ out,
+                                                               int nN, int nTiles, LnFold ln)
 {
-    // X ring: 2 stages of 32 KiB at BM 256, 4 of 16 KiB at BM 128 (64 KiB per workgroup)
-    constexpr int NS = BM == 256 ? 2 : 4;
-    const int nN = (W.N + 127) / 128, nTiles = (M / BM) * nN;
+    __shared__ __attribute__((aligned(16))) char smem[NS * BM * ZK * 2];
+    gemmz_body<FMT, EPI, NW, BM, NS>(smem, blockIdx.x, W, X, bias, res, out, nN, nTiles, ln);
+}
+
+template <int FMT, int NW, int BM, int NS>
+void dispatch_z(const DevWeight &W, const h16 *x, int M, const float *bias, int epi, const void *res, void *out,
+                hipStream_t s, const LnFold &ln)
+{
+    constexpr int BN = 32 * NW;
+    const int nN = (W.N + BN - 1) / BN, nTiles = (M / BM) * nN;
     if (epi == EPI_BIAS_F16)
-        gemmqv_kernel<FMT, EPI_BIAS_F16, BM, NS><<<nTiles, 256, 0, s>>>(W, x, bias, res, out, nN, nTiles, rln);
+        gemmz_kernel<FMT, EPI_BIAS_F16, NW, BM, NS><<<nTiles, 64 * NW, 0, s>>>(W, x, bias, res, out, nN, nTiles, ln);
     else if (epi == EPI_BIAS_GELU_F16)
-        gemmqv_kernel<FMT, EPI_BIAS_GELU_F16, BM, NS><<<nTiles, 256, 0, s>>>(W, x, bias, res, out, nN, nTiles, rln);
+        gemmz_kernel<FMT, EPI_BIAS_GELU_F16, NW, BM, NS><<<nTiles, 64 * NW, 0, s>>>(W, x, bias, res, out, nN, nTiles,
+                                                                                   ln);
     else
-        gemmqv_kernel<FMT, EPI_BIAS_RES, BM, NS><<<nTiles, 256, 0, s>>>(W, x, bias, res, out, nN, nTiles, rln);
+        gemmz_kernel<FMT, EPI_BIAS_RES, NW, BM, NS><<<nTiles, 64 * NW, 0, s>>>(W, x, bias, res, out, nN, nTiles, ln);
+}
+
+// Co-resident 4-wave workgroups the device holds at once (two per CU).
+int z_slots()
+{
+    static const int slots = [] {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        return 2 * cus;
+    }();
+    return slots;
+}
+
+template <int FMT>
+void launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, int32_t epi, const void *res,
+                void *out, hipStream_t s, const LnFold &ln, int cfg)
+{
+    if (cfg == 0) {
+        // measured in the forward at C3 (profiles/r01_gemm16_sweep.log): 256 x 128
+        // tiles two per CU beat 128 x 128 once there are two such tiles per CU
+        const bool fills = M % 256 == 0 && (long)(M / 256) * (W.N / 128) >= z_slots();
+        cfg = fills ? 2 : 3;
+    }
+    if (cfg == 2 && M % 256 == 0) dispatch_z<FMT, 4, 256, 2>(W, x, M, bias, epi, res, out, s, ln);
+    else dispatch_z<FMT, 4, 128, 4>(W, x, M, bias, epi, res, out, s, ln);
 }
 
 }  // namespace
 
-// Diagnostics: q4_0 gemmqw with per-wave s_memtime stamps (4 per wave) into `stamps`
-// (device buffer of nTiles * 8 * 4 uint64).  Returns the tile count.
-int launch_gemm_q_stamped(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi,
-                          const void *res, void *out, hipStream_t s, int32_t wm, uint64_t *stamps, int32_t diag)
-{
-    const h16 *x = (const h16 *)X;
-    const int BN = 256 / wm;
-    if (wm == 1) {
-        // stamps == nullptr: the same variant without the stamps (for timing)
-        auto qwd = [&](auto dtag) {
-            constexpr int D = decltype(dtag)::value;
-            if (stamps) dispatch_qw<FMT_Q4_0, 1, D | 0x10>(W, x, M, bias, epi, res, out, s, ResLN(), stamps);
-            else dispatch_qw<FMT_Q4_0, 1, D>(W, x, M, bias, epi, res, out, s, ResLN(), nullptr);
-        };
-        switch (diag) {
-        case 1: qwd(std::integral_constant<int, 0x1>()); break;
-        case 2: qwd(std::integral_constant<int, 0x2>()); break;
-        case 3: qwd(std::integral_constant<int, 0x3>()); break;
-        case 4: qwd(std::integral_constant<int, 0x4>()); break;
-        case 8: qwd(std::integral_constant<int, 0x8>()); break;
-        case 15: qwd(std::integral_constant<int, 0xf>()); break;
-        case 256: qwd(std::integral_constant<int, 0x100>()); break;
-        default: qwd(std::integral_constant<int, 0>()); break;
-        }
-    } else if (wm == 2) {
-        dispatch_qw<FMT_Q4_0, 2, 0x10>(W, x, M, bias, epi, res, out, s, ResLN(), stamps);
-    } else {   // wm 4: gemmqv BM 256, wm 5: gemmqv BM 128 (4 waves per tile)
-        const int BM = wm == 4 ? 256 : 128;
-        const int nN = (W.N + 127) / 128, nt = (M / BM) * nN;
-        auto go = [&](auto kern) { kern<<<nt, 256, 0, s>>>(W, x, bias, res, out, nN, nt, ResLN(), stamps); };
-        if (wm == 4) {
-            if (epi == EPI_BIAS_F16) go(gemmqv_kernel<FMT_Q4_0, EPI_BIAS_F16, 256, 2, true>);
-            else if (epi == EPI_BIAS_GELU_F16) go(gemmqv_kernel<FMT_Q4_0, EPI_BIAS_GELU_F16, 256, 2, true>);
-            else go(gemmqv_kernel<FMT_Q4_0, EPI_BIAS_RES, 256, 2, true>);
-        } else {
-            if (epi == EPI_BIAS_F16) go(gemmqv_kernel<FMT_Q4_0, EPI_BIAS_F16, 128, 4, true>);
-            else if (epi == EPI_BIAS_GELU_F16) go(gemmqv_kernel<FMT_Q4_0, EPI_BIAS_GELU_F16, 128, 4, true>);
-            else go(gemmqv_kernel<FMT_Q4_0, EPI_BIAS_RES, 128, 4, true>);
-        }
-        return nt * 4 / 8;   // in units of 8 waves
-    }
-    return (M / GM) * ((W.N + BN - 1) / BN);
-}
-
-int g_gemm_variant = 0;   // 0: heuristic (gemmqv, gemmqw for the GELU form), 2: gemmqw -- A/B benches
-int g_force_bn = 0;       // tests: force the tile shape (128 / 256; 0 = heuristic)
-
-template <int FMT>
-void launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, int32_t epi, const void *res,
-                void *out, hipStream_t s, const ResLN &rln)
-{
-    const int force = g_force_bn;
-    int variant = g_gemm_variant;
-    // measured (profiles/r01_gemm_sweep.log): the GELU form is fastest as gemmqw
-    // (one 8-wave workgroup per CU), the others as gemmqv (two per CU)
-    if (variant == 0 && epi == EPI_BIAS_GELU_F16 && !force && W.N % 256 == 0 &&
-        (long)(M / GM) * (W.N / 256) >= 512)
-        variant = 2;
-    if (variant == 2) {
-        const bool wide = force ? force == 256 : (W.N % 256 == 0 && (long)(M / GM) * (W.N / 256) >= 512);
-        if (wide) dispatch_qw<FMT, 1>(W, x, M, bias, epi, res, out, s, rln);
-        else dispatch_qw<FMT, 2>(W, x, M, bias, epi, res, out, s, rln);
-        return;
-    }
-    // 2 workgroups / CU; BM 128 for the residual (f32) form and for small M
-    const bool big = force ? force == 256 : (epi != EPI_BIAS_RES && M >= 256 * 64);
-    if (big) dispatch_qv<FMT, 256>(W, x, M, bias, epi, res, out, s, rln);
-    else dispatch_qv<FMT, 128>(W, x, M, bias, epi, res, out, s, rln);
-}
+int g_gemm_cfg = 0;
 
 int launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi, const void *res,
-                void *out, hipStream_t s, const ResLN &rln)
+                void *out, hipStream_t s, const LnFold &ln)
 {
-    if (W.layout == 1) return launch_gemm16(W, X, M, bias, epi, res, out, s, rln);
     const h16 *x = (const h16 *)X;
+    if (W.N % 32 || W.K % ZK || M % 128) return -1;
+    const int cfg = g_gemm_cfg;
     switch (W.fmt) {
-    case FMT_Q4_0: launch_fmt<FMT_Q4_0>(W, x, M, bias, epi, res, out, s, rln); break;
-    case FMT_Q4_1: launch_fmt<FMT_Q4_1>(W, x, M, bias, epi, res, out, s, rln); break;
-    case FMT_Q8_0: launch_fmt<FMT_Q8_0>(W, x, M, bias, epi, res, out, s, rln); break;
-    default: launch_fmt<FMT_F16>(W, x, M, bias, epi, res, out, s, rln); break;
+    case FMT_Q4_0: launch_fmt<FMT_Q4_0>(W, x, M, bias, epi, res, out, s, ln, cfg); break;
+    case FMT_Q4_1: launch_fmt<FMT_Q4_1>(W, x, M, bias, epi, res, out, s, ln, cfg); break;
+    case FMT_Q8_0: launch_fmt<FMT_Q8_0>(W, x, M, bias, epi, res, out, s, ln, cfg); break;
+    default: launch_fmt<FMT_F16>(W, x, M, bias, epi, res, out, s, ln, cfg); break;
     }
     return 0;
 }

@@ -68,6 +68,8 @@ bool load_model_file(const char *path, HostModel &m, std::string &err, bool verb
 
 // Dequantize one row of k elements into f32.
 void dequant_row(int fmt, const uint8_t *src, float *dst, int64_t k);
+// One row of k values in file format `fmt` (the quantizer's block rules).
+void quantize_row(int fmt, const float *x, uint8_t *dst, int64_t k);
 
 // Native quantizer (mirrors models/quantize.cpp:27-268; itype 2, 3, or 8).
 int quantize_file(const char *in, const char *out, int itype, bool verbose);

@@ -277,6 +277,16 @@ static void quant_block(int itype, const float *x, uint8_t *o)
     }
 }
 
+void quantize_row(int fmt, const float *x, uint8_t *dst, int64_t k)
+{
+    if (fmt == FMT_F32) { std::memcpy(dst, x, (size_t)k * 4); return; }
+    if (fmt == FMT_F16) {
+        for (int64_t i = 0; i < k; ++i) { const uint16_t h = f32_to_f16(x[i]); std::memcpy(dst + 2 * i, &h, 2); }
+        return;
+    }
+    for (int64_t b = 0; b < k / QK; ++b) quant_block(fmt, x + QK * b, dst + fmt_block_bytes(fmt) * (size_t)b);
+}
+
 int quantize_file(const char *in, const char *out, int itype, bool verbose)
 {
     if (itype != FMT_Q4_0 && itype != FMT_Q4_1 && itype != FMT_Q8_0) {

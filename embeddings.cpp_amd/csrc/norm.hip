@@ -1,10 +1,10 @@
-// Memory-bound row kernels: embeddings + LayerNorm, LayerNorm, mean pool + L2.
-// One wave per token row; each lane owns 4 consecutive features per 256-wide
-// slice (16-B loads and stores), reductions by wave shuffles.
+// Memory-bound row kernels: embeddings + LayerNorm, the LayerNorm statistics
+// of the residual stream, mean pool + L2 (the LN fold of kernels.h).
+// Embeddings: one wave per token row; each lane owns 4 consecutive features per
+// 256-wide slice (16-B loads and stores), reductions by wave shuffles.
 #include "device_common.h"
 #include "host_common.h"
 #include "kernels.h"
-#include "rowln.h"
 
 #include <cmath>
 
@@ -52,9 +52,8 @@ __device__ __forceinline__ f32x4 table4(const DevTable &t, int row, int c)
 }
 
 __global__ __launch_bounds__(256) void embed_ln_kernel(DevTable word, DevTable type, DevTable pos,
-                                                       const float *__restrict__ ln_w, const float *__restrict__ ln_b,
-                                                       const int32_t *__restrict__ ids, const int32_t *__restrict__ cu,
-                                                       int d, h16 *__restrict__ yh, h16 *__restrict__ xh,
+                                                       const float *__restrict__ ln_w, const int32_t *__restrict__ ids,
+                                                       const int32_t *__restrict__ cu, int d, h16 *__restrict__ z,
                                                        float2 *__restrict__ stats)
 {
     const int b = blockIdx.y, lane = threadIdx.x & 63;
@@ -63,95 +62,67 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(DevTable word, DevTable t
     if (i >= len) return;
     const int t = start + i, id = ids[t];
     f32x4 v[MAXV];
+    float s = 0.f;
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) {
         const int c = 4 * (lane + 64 * k);
         if (c < d) {
-            // pos + (type[0] + word[id])  (bert.cpp:968-973 operand order)
+            // pos + (type[0] + word[id])  (bert.cpp:968-973 operand order), f32
             const f32x4 w = table4(word, id, c), ty = table4(type, 0, c), p = table4(pos, i, c);
-            h16x4 v16;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                v16[e] = (h16)(p[e] + (ty[e] + w[e]));
-                v[k][e] = (float)v16[e];       // LN of the stored (f16) residual value
-            }
-            *(h16x4 *)(yh + (size_t)t * d + c) = v16;            // pre-LN residual stream
+            for (int e = 0; e < 4; ++e) v[k][e] = p[e] + (ty[e] + w[e]);
+            s += (v[k][0] + v[k][1]) + (v[k][2] + v[k][3]);
         }
     }
-    ln_row<MAXV>(v, d, lane, ln_w, ln_b, xh + (size_t)t * d, stats + t);
-}
-
-// 32 rows per 256-thread block, 8 lanes per row (as layernorm_kernel): lane sub
-// of a row group gathers the 16-B chunks at features 8 sub + 64 k of the three
-// tables, so a wave has 8 rows' gathers in flight (the one-wave-per-row kernel
-// above has one), then ln8_row normalises the f16-rounded residual row.
-__global__ __launch_bounds__(256) void embed_ln8_kernel(DevTable word, DevTable type, DevTable pos,
-                                                        const float *__restrict__ ln_w, const float *__restrict__ ln_b,
-                                                        const int32_t *__restrict__ ids, const int32_t *__restrict__ cu,
-                                                        int d, h16 *__restrict__ yh, h16 *__restrict__ xh,
-                                                        float2 *__restrict__ stats)
-{
-    const int b = blockIdx.y, sub = threadIdx.x & 7;
-    const int i = blockIdx.x * 32 + (threadIdx.x >> 3);
-    const int start = cu[b], len = cu[b + 1] - start;
-    const bool valid = i < len;
-    const int t = start + (valid ? i : 0);
-    h16x8 v[16];
+    // ggml_norm (eps 1e-5, mean then centred variance; bert.cpp:977-984) of the f32 row
+    const float mean = wave_sum(s) / (float)d;
+    float s2 = 0.f;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) v[k] = h16x8{};
-    if (valid) {
-        const int id = ids[t];
+    for (int k = 0; k < MAXV; ++k) {
+        const int c = 4 * (lane + 64 * k);
+        if (c < d) {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const int c = 8 * sub + 64 * k;
-            if (64 * k >= d) continue;
-#pragma unroll
-            for (int hf = 0; hf < 2; ++hf) {
-                // pos + (type[0] + word[id])  (bert.cpp:968-973 operand order)
-                const f32x4 w = table4(word, id, c + 4 * hf), ty = table4(type, 0, c + 4 * hf),
-                            p = table4(pos, i, c + 4 * hf);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[k][4 * hf + e] = (h16)(p[e] + (ty[e] + w[e]));
-            }
-            *(h16x8 *)(yh + (size_t)t * d + c) = v[k];       // pre-LN residual stream
+            for (int e = 0; e < 4; ++e) { const float u = v[k][e] - mean; s2 += u * u; }
         }
     }
-    ln8_row<16>(v, t, valid, d, sub, ln_w, ln_b, xh, stats);
+    const float r = 1.0f / sqrtf(wave_sum(s2) / (float)d + 1e-5f);
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+        const int c = 4 * (lane + 64 * k);
+        if (c >= d) continue;
+        const f32x4 g = *(const f32x4 *)(ln_w + c);
+        h16x4 zh;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) zh[e] = (h16)(v[k][e] * g[e]);
+        *(h16x4 *)(z + (size_t)t * d + c) = zh;       // the stream as z = y * gamma (kernels.h LN fold)
+    }
+    if (lane == 0) stats[t] = float2{mean, r};
 }
 
-// 32 rows per 256-thread block, 8 lanes per row (rowln.h ln8_*: the same
-// arithmetic as the panel LN fused into the residual GEMM)
-__global__ __launch_bounds__(256) void layernorm_kernel(const h16 *__restrict__ y, int T, int d,
-                                                        const float *__restrict__ w, const float *__restrict__ b,
-                                                        h16 *__restrict__ xh, float2 *__restrict__ stats)
+// Row statistics from the residual GEMM's 32-feature group partials (sum, M2 about
+// the group mean): mean = sum / d, M2 = sum_g M2_g + (s_g - 32 mean)^2 / 32 (Chan et al.)
+__global__ __launch_bounds__(256) void ln_stats_kernel(const float2 *__restrict__ part, int G, int stride, int rows,
+                                                       int d, float2 *__restrict__ stats)
 {
-    const int lane = threadIdx.x & 63;
-    const int t = blockIdx.x * 32 + (threadIdx.x >> 3);
-    h16x8 v[16];
-    ln8_load<16>(y, t, t < T, d, lane & 7, v);
-    ln8_row<16>(v, t, t < T, d, lane & 7, w, b, xh, stats);
-}
-
-// Persistent form (A/B via BERT_LN_BLOCKS, measured slower): block b normalises
-// the 32-aligned row range [b rpb, min(T, (b + 1) rpb)), its 4 waves 8 rows each
-// per pass with the next pass's loads issued before this pass's arithmetic
-// (rowln.h ln_rows), so the reads and writes of one launch overlap.  The same
-// ln8_row arithmetic as the one-pass kernel above, so the same bits.
-template <int NCH>
-__global__ __launch_bounds__(256) void layernorm_rows_kernel(const h16 *__restrict__ y, int T, int d, int rpb,
-                                                             const float *__restrict__ w, const float *__restrict__ b,
-                                                             h16 *__restrict__ xh, float2 *__restrict__ stats)
-{
-    const int r0 = blockIdx.x * rpb;
-    ln_rows<NCH, 4>(y, r0, min(T, r0 + rpb), d, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), threadIdx.x & 63,
-                    w, b, xh, stats);
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= rows) return;
+    float s = 0.f;
+    for (int g = 0; g < G; ++g) s += part[(size_t)g * stride + t].x;
+    const float mean = s / (float)d;
+    float m2 = 0.f;
+    for (int g = 0; g < G; ++g) {
+        const float2 p = part[(size_t)g * stride + t];
+        const float dm = p.x - 32.0f * mean;
+        m2 += p.y + dm * dm * (1.0f / 32.0f);
+    }
+    stats[t] = float2{mean, 1.0f / sqrtf(m2 / (float)d + 1e-5f)};
 }
 
 // pool stage 1: partial column sums of 64-token chunks, weights 1/len
 // (bert.cpp:1087-1089: sum_i X[i][c] * (1/len)).
 constexpr int POOL_CHUNK = 64;
 
-__global__ __launch_bounds__(256) void pool_partial_kernel(const h16 *__restrict__ y32, const float2 *__restrict__ stats,
+__global__ __launch_bounds__(256) void pool_partial_kernel(const h16 *__restrict__ z, const float2 *__restrict__ stats,
                                                            const float *__restrict__ lw, const float *__restrict__ lb,
                                                            const int32_t *__restrict__ cu, int d, int n_chunks,
                                                            float *__restrict__ part)
@@ -172,12 +143,14 @@ __global__ __launch_bounds__(256) void pool_partial_kernel(const h16 *__restrict
         const f32x4 b0 = *(const f32x4 *)(lb + c), b1 = *(const f32x4 *)(lb + c + 4);
 #pragma unroll 4
         for (int i = i0 + tl; i < i1; i += TT) {
-            const h16x8 y = *(const h16x8 *)(y32 + (size_t)(start + i) * d + c);
+            const h16x8 y = *(const h16x8 *)(z + (size_t)(start + i) * d + c);
             const float2 st = stats[start + i];
+            const float r = st.y, t0 = -st.x * st.y;
+            // LN(y) = r z - r mean gamma + beta (kernels.h LN fold)
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                a0[e] += ln_apply((float)y[e], st.x, st.y, w0[e], b0[e]) * wt;
-                a1[e] += ln_apply((float)y[4 + e], st.x, st.y, w1[e], b1[e]) * wt;
+                a0[e] += fmaf(r, (float)y[e], fmaf(t0, w0[e], b0[e])) * wt;
+                a1[e] += fmaf(r, (float)y[4 + e], fmaf(t0, w1[e], b1[e])) * wt;
             }
         }
     }
@@ -238,61 +211,26 @@ void launch_count_nonfinite(const void *p, size_t n, int f16, unsigned *cnt, hip
 }
 
 void launch_embed_ln(const DevTable &word, const DevTable &type, const DevTable &pos, const float *ln_w,
-                     const float *ln_b, const int32_t *ids, const int32_t *cu, int32_t n_seqs, int32_t max_len,
-                     int32_t d, uint16_t *yh, uint16_t *xh, float2 *stats, hipStream_t s)
+                     const int32_t *ids, const int32_t *cu, int32_t n_seqs, int32_t max_len, int32_t d, uint16_t *z,
+                     float2 *stats, hipStream_t s)
 {
-    // the one-wave-per-row kernel by default; BERT_EMBED_LN8=1 (A/B) runs the
-    // 8-lanes-per-row form, measured no faster (53.0 vs 51.9 us at C3, gpurun_out r01j:
-    // the table gathers, not the row sums, bound it)
-    static const bool rowwave = [] { const char *e = std::getenv("BERT_EMBED_LN8"); return !(e && *e == '1'); }();
-    if (rowwave) {
-        dim3 grid((max_len + 3) / 4, n_seqs);
-        embed_ln_kernel<<<grid, 256, 0, s>>>(word, type, pos, ln_w, ln_b, ids, cu, d, (h16 *)yh, (h16 *)xh, stats);
-        return;
-    }
-    dim3 grid((max_len + 31) / 32, n_seqs);
-    embed_ln8_kernel<<<grid, 256, 0, s>>>(word, type, pos, ln_w, ln_b, ids, cu, d, (h16 *)yh, (h16 *)xh, stats);
+    dim3 grid((max_len + 3) / 4, n_seqs);
+    embed_ln_kernel<<<grid, 256, 0, s>>>(word, type, pos, ln_w, ids, cu, d, (h16 *)z, stats);
 }
 
-void launch_layernorm(const uint16_t *yh, int32_t T, int32_t d, const float *w, const float *b, uint16_t *xh,
-                      float2 *stats, hipStream_t s)
+void launch_ln_stats(const float2 *part, int32_t G, int32_t stride, int32_t rows, int32_t d, float2 *stats,
+                     hipStream_t s)
 {
-    if (T <= 0) return;
-    // BERT_LN_BLOCKS (A/B): n > 0 runs the persistent form on n blocks (-1: two per
-    // CU); default the one-pass kernel, measured faster in the forward at C3
-    // (gpurun_out r01h: 21.8 vs 22.7 us at two blocks per CU)
-    static const int nblk = [] {
-        const char *e = std::getenv("BERT_LN_BLOCKS");
-        const int n = e ? std::atoi(e) : 0;
-        if (n >= 0) return n;
-        int dev = 0, cus = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-            cus = 256;
-        return 2 * cus;
-    }();
-    if (nblk <= 0) {
-        layernorm_kernel<<<(T + 31) / 32, 256, 0, s>>>((const h16 *)yh, T, d, w, b, (h16 *)xh, stats);
-        return;
-    }
-    const int rpb = ((T + nblk - 1) / nblk + 31) & ~31;
-    const int grid = (T + rpb - 1) / rpb;
-    const h16 *y = (const h16 *)yh;
-    h16 *o = (h16 *)xh;
-    switch (d / 64) {
-    case 6: layernorm_rows_kernel<6><<<grid, 256, 0, s>>>(y, T, d, rpb, w, b, o, stats); break;
-    case 12: layernorm_rows_kernel<12><<<grid, 256, 0, s>>>(y, T, d, rpb, w, b, o, stats); break;
-    default: layernorm_rows_kernel<16><<<grid, 256, 0, s>>>(y, T, d, rpb, w, b, o, stats); break;
-    }
+    if (rows > 0) ln_stats_kernel<<<(rows + 255) / 256, 256, 0, s>>>(part, G, stride, rows, d, stats);
 }
 
 int32_t pool_chunks(int32_t max_len) { return (max_len + POOL_CHUNK - 1) / POOL_CHUNK; }
 
-void launch_pool_l2(const uint16_t *yh, const ResLN &ln, const int32_t *cu, int32_t n_seqs, int32_t max_len,
-                    int32_t d, float *partial, float *out, hipStream_t s)
+void launch_pool_l2(const uint16_t *z, const float2 *stats, const float *ln_w, const float *ln_b, const int32_t *cu,
+                    int32_t n_seqs, int32_t max_len, int32_t d, float *partial, float *out, hipStream_t s)
 {
     const int nc = pool_chunks(max_len);
-    pool_partial_kernel<<<dim3(nc, n_seqs), 256, 0, s>>>((const h16 *)yh, ln.stats, ln.w, ln.b, cu, d, nc, partial);
+    pool_partial_kernel<<<dim3(nc, n_seqs), 256, 0, s>>>((const h16 *)z, stats, ln_w, ln_b, cu, d, nc, partial);
     pool_final_kernel<<<n_seqs, 256, 0, s>>>(partial, d, nc, out);
 }
 

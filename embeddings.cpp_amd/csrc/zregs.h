@@ -1,5 +1,5 @@
-// Lane-order weight fragments (kernels.h layout 1) for the 16x16x32 f16 MFMA
-// kernels (gemm16.hip): one lane's raw words of one K-step (64 k,
+// Lane-order weight fragments (kernels.h) for the 16x16x32 f16 MFMA
+// GEMM (gemm.hip): one lane's raw words of one K-step (64 k,
 // fragments u = 2a + s: features +16a, k-slice s) and their dequantization to
 // f16 A fragments, (q - 8) d (q4_0), q d + m (q4_1), q d (q8_0) rounded once;
 // and the permlane16 row exchange of the epilogues.

@@ -66,53 +66,51 @@ BERT_API int32_t bertx_quantize_file(const char *fname_in, const char *fname_out
 BERT_API int32_t bertx_convert_hf(const char *dir_model, const char *fname_out, int32_t ftype);
 
 /*
- * Per-kernel parity hooks (host buffers in/out, runs synchronously on the
- * first device).  w_rows: the weight exactly as the model file stores it
- * (N rows of K elements in format `fmt` = 0,1,2,3,8).  x: f16 bits [M][K].
- * epi: 0 = +bias -> f16, 1 = +bias, GELU -> f16, 2 = +bias +res -> f16 (res f16 [M][N],
- * the residual-stream form; sum in f32).
- * tile_n: 0 = the production kernel and weight layout; 128 / 256 = gemm.hip
- * (32x32x16 MFMA, weight layout 0) with that tile width; 0x1000 | c = gemm16.hip
- * (16x16x32 MFMA, weight layout 1) with tile config c (0 heuristic, 1 = 8 waves
- * 256x256, 2 = 4 waves 256x128, 3 = 4 waves 128x128).
+ * Per-kernel parity hooks (host buffers in/out, run synchronously on device 0).
+ * w_rows: the weight exactly as the model file stores it (N rows of K elements
+ * in format `fmt` = 0,1,2,3,8).  x: f16 bits [M][K].  epi: 0 = +bias -> f16,
+ * 1 = +bias, era GELU -> f16, 2 = +bias +res -> f16 (res f16 [M][N], the
+ * residual-stream form; sum in f32, computed in place over res).  cfg: GEMM tile
+ * config (0 = the production heuristic, 2 = 4 waves 256x128, 3 = 4 waves 128x128).
+ * Reference interface these kernels replace: ggml_mul_mat + ggml_add (+ ggml_gelu)
+ * at bert.cpp:994-1016, 1040-1045, 1059-1072.
  */
 BERT_API int32_t bertx_test_gemm(int32_t fmt, int32_t N, int32_t K, const void *w_rows,
                                  const float *bias, int32_t M, const uint16_t *x,
-                                 int32_t epi, const void *res, void *out, int32_t tile_n);
+                                 int32_t epi, const void *res, void *out, int32_t cfg);
 
 /*
- * Residual projection + the LayerNorm that follows it (bert.cpp:1040-1056 and
- * 1070-1082), host buffers, device 0, gemm16 weights: out f16 [M][N] =
- * LN(res) + x W^T + bias, with LN(res) from (stats [M] (mean, 1/sigma) as float
- * pairs, lnw, lnb) or res itself when stats is NULL; then xh f16 [M][N] =
- * LN(out) with (nw, nb) and st_out [M] its (mean, 1/sigma), for the first `rows`
- * rows.  panel = 1: the LN runs inside the GEMM (ResLN panel form, -2 if the
- * shape has none); 0: the separate LN kernel.  Both must give the same bits.
+ * The same GEMM with the LayerNorm bookkeeping of the forward (the "LN fold",
+ * DESIGN.md §2; LayerNorm = bert.cpp:977-984, 1048-1056, 1074-1082):
+ *  - in_stats (epi 0/1): x holds z = y * in_g of rows y with in_stats[M] =
+ *    (mean, 1/sigma) float pairs; the result is LN(y) W^T + bias with LN's gamma
+ *    in_g, beta in_b [K] (else NULL: plain x W^T + bias);
+ *  - epi 2: res holds z = y * res_g with res_stats [M] (the residual is LN(y) with
+ *    gamma res_g, beta res_b [N]), or the plain residual when res_stats is NULL;
+ *    with g_next [N] the output is f16(y' * g_next) of the new stream y' =
+ *    residual + x W^T + bias and st_out [M] receives y''s (mean, 1/sigma) as the
+ *    forward computes them (epilogue partials + the statistics kernel).
  */
 BERT_API int32_t bertx_test_gemm_ln(int32_t fmt, int32_t N, int32_t K, const void *w_rows, const float *bias,
-                                    int32_t M, int32_t rows, const uint16_t *x, const uint16_t *res,
-                                    const float *stats, const float *lnw, const float *lnb, const float *nw,
-                                    const float *nb, uint16_t *out, uint16_t *xh, float *st_out, int32_t panel);
+                                    int32_t M, const uint16_t *x, const float *in_stats, const float *in_g,
+                                    const float *in_b, int32_t epi, const uint16_t *res, const float *res_stats,
+                                    const float *res_g, const float *res_b, const float *g_next, uint16_t *out,
+                                    float *st_out, int32_t cfg);
 
 /*
  * GEMM micro-benchmark on random operands (device 0): average device time of
- * `iters` launches of the GEMM for fmt / N / K / M / epi.  tile_n: 0 / 128 / 256 =
- * gemm.hip (layout 0) heuristic / tile width; 0x1000 | c = gemm16.hip config c (as
- * bertx_test_gemm).  ablate: -1 = production kernels; -2 = the one-workgroup-
- * per-CU kernel (gemmqw) for every form; -3 - d (q4_0, tile_n 0 or 256) = a
- * diagnostic gemmqw build: one launch with per-wave s_memtime phase stamps
- * (printed to stderr), then the timed launches of the same build without stamps;
- * d = ablation bits (1 no dequant, 2 no B reads, 4 no K-loop barrier, 8 no MFMA)
- * or 256 (B reads software-pipelined two ahead).
+ * `iters` launches of the GEMM for fmt / N / K / M / epi / cfg (as
+ * bertx_test_gemm), in the forward's own forms: the LN fold on the input of
+ * epi 0/1, the residual LN + next gamma + partial statistics for epi 2.
  */
-BERT_API int32_t bertx_bench_gemm(int32_t fmt, int32_t N, int32_t K, int32_t M, int32_t epi, int32_t tile_n,
-                                  int32_t ablate, int32_t iters, float *avg_us);
+BERT_API int32_t bertx_bench_gemm(int32_t fmt, int32_t N, int32_t K, int32_t M, int32_t epi, int32_t cfg,
+                                  int32_t iters, float *avg_us);
 
 /*
  * Attention micro-benchmark on random operands (device 0): average device time
  * of `iters` launches for n_seqs sentences of `len` tokens, n_head heads of size
- * dh; variant 0 = production kernel, 1 = the previous one, others: A/B builds
- * (launch_attention in attention.hip).
+ * dh; variant 0 = the production kernel, 7 = the same on at most 7 workgroups
+ * (many ragged items per workgroup).
  */
 BERT_API int32_t bertx_bench_attention(int32_t n_seqs, int32_t len, int32_t n_head, int32_t dh, int32_t variant,
                                        int32_t iters, float *avg_us);

@@ -5,7 +5,7 @@ OUT=$GRAFT_REPO_ROOT/gpurun_out/${TAG:-gpmc}
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp
-for cfg in ${CFGS:-0x1002 0x1006}; do
+for cfg in ${CFGS:-0}; do
   i=0
   while read -r grp; do
     [ -z "$grp" ] && continue

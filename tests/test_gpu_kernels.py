@@ -1,5 +1,6 @@
-"""Per-kernel parity on the GPU: the fused dequant GEMM (bertx_test_gemm) against a numpy
-fp32/f64 reference of the same op, for every weight format and epilogue."""
+"""Per-kernel parity on the GPU: the fused dequant GEMM (bertx_test_gemm / bertx_test_gemm_ln)
+against a numpy f64 reference of the same op, for every weight format and epilogue, in the
+forward's own LayerNorm-fold forms (kernels.h); the attention kernels against numpy."""
 import ctypes
 
 import numpy as np
@@ -33,7 +34,7 @@ def weight_rows(fmt, W):
     return b"".join(rows), deq
 
 
-def run_gemm(lib, fmt, W, bias, X, epi, res=None, tile_n=0):
+def run_gemm(lib, fmt, W, bias, X, epi, res=None, cfg=0):
     N, K = W.shape
     M = X.shape[0]
     wb, deq = weight_rows(fmt, W)
@@ -44,25 +45,26 @@ def run_gemm(lib, fmt, W, bias, X, epi, res=None, tile_n=0):
         res = np.ascontiguousarray(res, np.float16)
         resp = res.ctypes.data
     rc = lib.bertx_test_gemm(fmt, N, K, wb, np.ascontiguousarray(bias, np.float32).ctypes.data_as(
-        ctypes.POINTER(ctypes.c_float)), M, xh.ctypes.data, epi, resp, out.ctypes.data, tile_n)
+        ctypes.POINTER(ctypes.c_float)), M, xh.ctypes.data, epi, resp, out.ctypes.data, cfg)
     assert rc == 0
     return out.astype(np.float32), deq, xh.astype(np.float32)
 
 
+def gelu_ref(acc):
+    """ggml-era GELU: tanh form on the f16-rounded input (bert.cpp:1063)."""
+    x16 = acc.astype(np.float16).astype(np.float64)
+    return 0.5 * x16 * (1 + np.tanh(0.7978845608028654 * x16 * (1 + 0.044715 * x16 * x16)))
+
+
 @pytest.mark.parametrize("fmt", sorted(FMTS))
 @pytest.mark.parametrize("epi", [0, 1, 2])
-@pytest.mark.parametrize("shape", [(192, 256, 300, 0), (768, 768, 512, 0), (512, 192, 700, 256),
-                                   (256, 3072, 256, 128),
-                                   # gemm16 (layout 1) configs: 0x1000 | 1 (8 waves 256x256),
-                                   # 2 (4 waves 256x128), 3 (4 waves 128x128)
-                                   (768, 768, 512, 0x1001), (2304, 768, 768, 0x1002), (448, 192, 700, 0x1003),
-                                   (256, 3072, 256, 0x1001),
-                                   # 0x1004: the ping-pong kernel (8 waves, 256 x 256, halves alternating)
-                                   (768, 768, 512, 0x1004), (512, 3072, 768, 0x1004), (2304, 192, 256, 0x1004)])
+@pytest.mark.parametrize("shape", [(192, 256, 300, 0), (768, 768, 512, 0), (512, 192, 700, 3),
+                                   (256, 3072, 256, 3),
+                                   # tile configs: 2 (4 waves 256x128), 3 (4 waves 128x128)
+                                   (768, 768, 512, 2), (2304, 768, 768, 2), (448, 192, 700, 3),
+                                   (256, 3072, 256, 2), (2304, 192, 256, 2)])
 def test_gemm_matches_numpy(lib, fmt, epi, shape):
-    N, K, M, tile_n = shape
-    if tile_n == 256 and epi == 2:   # gemm.hip's 256-wide tile has no residual form
-        pytest.skip("the residual epilogue runs 128 wide")
+    N, K, M, cfg = shape
     rng = np.random.default_rng(fmt * 10 + epi)
     W = rng.standard_normal((N, K)).astype(np.float32) * 0.05
     W[:, 5] *= 20.0                       # asymmetric outliers catch transposed maps
@@ -70,7 +72,7 @@ def test_gemm_matches_numpy(lib, fmt, epi, shape):
     X = rng.standard_normal((M, K)).astype(np.float32)
     X[7] *= 3.0
     res = rng.standard_normal((M, N)).astype(np.float16) if epi == 2 else None
-    got, deq, xh = run_gemm(lib, fmt, W, bias, X, epi, res, tile_n)
+    got, deq, xh = run_gemm(lib, fmt, W, bias, X, epi, res, cfg)
     # the kernel multiplies f16 operands with f32 accumulation: reference uses f16(weights)
     wref = deq.astype(np.float16).astype(np.float64)
     acc = xh.astype(np.float64) @ wref.T + bias.astype(np.float64)
@@ -78,8 +80,7 @@ def test_gemm_matches_numpy(lib, fmt, epi, shape):
         ref = acc
         tol = 2e-3 * np.abs(ref).max()
     elif epi == 1:
-        x16 = acc.astype(np.float16).astype(np.float64)
-        ref = 0.5 * x16 * (1 + np.tanh(0.7978845608028654 * x16 * (1 + 0.044715 * x16 * x16)))
+        ref = gelu_ref(acc)
         tol = 3e-3 * np.abs(ref).max()
     else:                                 # f32 sum of the f16 residual, rounded to f16
         ref = res.astype(np.float64) + acc
@@ -92,79 +93,94 @@ def test_gemm_matches_numpy(lib, fmt, epi, shape):
         assert np.abs(got - exact).max() <= 5e-3 * np.abs(exact).max()
 
 
-@pytest.mark.parametrize("N,K,M,epi", [(2304, 768, 8192, 0), (3072, 768, 8192, 1), (768, 3072, 32768, 2)])
-def test_gemm_column_split_bitwise(lib, N, K, M, epi):
-    """gemm16's column split (gemmz_split_kernel, chosen by the heuristic when a grid of
-    256 x 128 tiles is not whole rounds of two per CU: its last columns run as 128 x 128
-    tiles in the same launch) gives the bits of the unsplit 256 x 128 grid, and numpy
-    within f16 rounding."""
-    rng = np.random.default_rng(N + K + epi)
-    W = rng.standard_normal((N, K)).astype(np.float32) * 0.05
-    bias = rng.standard_normal(N).astype(np.float32) * 0.1
-    X = rng.standard_normal((M, K)).astype(np.float32)
-    res = rng.standard_normal((M, N)).astype(np.float16) if epi == 2 else None
-    split, deq, xh = run_gemm(lib, 2, W, bias, X, epi, res, 0x1005)     # split grid
-    whole, _, _ = run_gemm(lib, 2, W, bias, X, epi, res, 0x1002)        # 256 x 128 everywhere
-    assert np.array_equal(split, whole)
-    acc = xh.astype(np.float64) @ deq.astype(np.float16).astype(np.float64).T + bias
-    if epi == 1:
-        x16 = acc.astype(np.float16).astype(np.float64)
-        ref = 0.5 * x16 * (1 + np.tanh(0.7978845608028654 * x16 * (1 + 0.044715 * x16 * x16)))
-    elif epi == 2:
-        ref = res.astype(np.float64) + acc
-    else:
-        ref = acc
-    assert np.abs(split - ref).max() <= 3e-3 * np.abs(ref).max()
-
-
-def ln_ref(y, w, b):
-    """ggml_norm (eps 1e-5, mean then centred variance) * w + b (bert.cpp:1048-1056) in f64."""
+def ln_ref(y):
+    """ggml_norm statistics (eps 1e-5, mean then centred variance; bert.cpp:1048-1056) in f64."""
     y = y.astype(np.float64)
-    mean = y.mean(axis=1, keepdims=True)
-    sc = 1.0 / np.sqrt(((y - mean) ** 2).mean(axis=1, keepdims=True) + 1e-5)
-    return (y - mean) * sc * w + b, mean[:, 0], sc[:, 0]
+    mean = y.mean(axis=1)
+    return mean, 1.0 / np.sqrt(((y - mean[:, None]) ** 2).mean(axis=1) + 1e-5)
 
 
-@pytest.mark.parametrize("fmt", [1, 2, 3, 8])
-@pytest.mark.parametrize("N,K,M,rows", [(768, 768, 512, 500), (384, 1536, 256, 256), (1024, 1024, 384, 257),
-                                        (768, 3072, 256, 129)])
-def test_residual_gemm_panel_layernorm(lib, fmt, N, K, M, rows):
-    """Residual projection + the following LN: the panel form fused into the GEMM
-    (the workgroup completing a 128-row panel normalises it) equals the separate
-    LN kernel bit for bit, and both match numpy (f64) within f16 rounding."""
-    rng = np.random.default_rng(fmt + N + rows)
+def f32p(a):
+    return None if a is None else np.ascontiguousarray(a, np.float32).ctypes.data
+
+
+@pytest.mark.parametrize("fmt", [0, 1, 2, 3, 8])
+@pytest.mark.parametrize("epi", [0, 1])
+@pytest.mark.parametrize("N,K,M,cfg", [(2304, 768, 512, 0), (384, 1536, 300, 3), (1024, 1024, 768, 2)])
+def test_gemm_input_ln_fold(lib, fmt, epi, N, K, M, cfg):
+    """Projection of a LayerNorm'd stream as the forward runs it (kernels.h LN fold):
+    the GEMM reads z = f16(y * gamma) and the row statistics of y, and returns
+    LN(y) W^T + b (then GELU for epi 1) -- numpy f64 within f16 rounding.  Rows
+    carry a large mean and outlier channels (the regime where folding the mean
+    out of the product could cancel)."""
+    rng = np.random.default_rng(fmt * 7 + epi + N)
     W = rng.standard_normal((N, K)).astype(np.float32) * 0.05
     wb, deq = weight_rows(fmt, W)
     bias = rng.standard_normal(N).astype(np.float32) * 0.1
+    y = rng.standard_normal((M, K)) * 2.0 + rng.standard_normal((M, 1)) * 3.0
+    y[:, 7] += 80.0
+    y[:, 300 % K] -= 150.0
+    g = (1.0 + rng.standard_normal(K) * 0.3).astype(np.float32)
+    g[7] = 0.3
+    be = (rng.standard_normal(K) * 0.1).astype(np.float32)
+    mean, r = ln_ref(y)
+    stats = np.ascontiguousarray(np.stack([mean, r], axis=1), np.float32)
+    z = np.ascontiguousarray((y * g).astype(np.float16))
+    out = np.zeros((M, N), np.float16)
+    rc = lib.bertx_test_gemm_ln(fmt, N, K, wb, f32p(bias), M, z.ctypes.data, stats.ctypes.data, f32p(g), f32p(be),
+                                epi, None, None, None, None, None, out.ctypes.data, None, cfg)
+    assert rc == 0
+    x = (y - mean[:, None]) * r[:, None] * g + be
+    acc = x @ deq.astype(np.float16).astype(np.float64).T + bias
+    if epi == 1:
+        ref = gelu_ref(acc)
+        tol = 3e-3 * np.abs(ref).max()
+    else:
+        ref = acc
+        tol = 2e-3 * np.abs(ref).max()
+    err = np.abs(out.astype(np.float64) - ref).max()
+    assert err <= tol, (FMTS[fmt], epi, err, tol)
+
+
+@pytest.mark.parametrize("fmt", [1, 2, 3, 8])
+@pytest.mark.parametrize("N,K,M,cfg", [(768, 768, 512, 0), (384, 1536, 256, 3), (1024, 1024, 384, 2),
+                                       (768, 3072, 256, 0)])
+def test_residual_gemm_ln_statistics(lib, fmt, N, K, M, cfg):
+    """Residual projection as the forward runs it: res = f16(y * gamma) with y's
+    statistics (the residual is LN(y)), y' = LN(y) + x W^T + b comes back as
+    f16(y' * g_next), and y''s (mean, 1/sigma) from the epilogue's 32-feature
+    partials + the statistics kernel match numpy's two-pass LN statistics."""
+    rng = np.random.default_rng(fmt + N + K)
+    W = rng.standard_normal((N, K)).astype(np.float32) * 0.05
+    wb, deq = weight_rows(fmt, W)
+    bias = rng.standard_normal(N).astype(np.float32) * 0.1
+    bias[11] += 60.0                        # an outlier channel of the new stream
     X = rng.standard_normal((M, K)).astype(np.float16)
-    res = (rng.standard_normal((M, N)) * 2 + 0.5).astype(np.float16)
-    mean = res.astype(np.float64).mean(axis=1)
-    stats = np.stack([mean, 1.0 / np.sqrt(res.astype(np.float64).var(axis=1) + 1e-5)], axis=1).astype(np.float32)
-    lnw, lnb, nw, nb = (rng.standard_normal(N).astype(np.float32) * s + o
-                        for s, o in ((0.1, 1.0), (0.1, 0.0), (0.2, 1.0), (0.1, 0.0)))
-    outs = []
-    for panel in (1, 0):
-        out = np.zeros((M, N), np.float16)
-        xh = np.zeros((M, N), np.float16)
-        st = stats.copy()
-        rc = lib.bertx_test_gemm_ln(fmt, N, K, wb, bias.ctypes.data, M, rows, X.ctypes.data, res.ctypes.data,
-                                    st.ctypes.data, lnw.ctypes.data, lnb.ctypes.data, nw.ctypes.data,
-                                    nb.ctypes.data, out.ctypes.data, xh.ctypes.data, st.ctypes.data, panel)
-        assert rc == 0, (panel, rc)
-        outs.append((out, xh, st))
-    (o1, x1, s1), (o0, x0, s0) = outs
-    assert np.array_equal(o1.view(np.uint16), o0.view(np.uint16))
-    assert np.array_equal(x1[:rows].view(np.uint16), x0[:rows].view(np.uint16))
-    assert np.array_equal(s1[:rows], s0[:rows])
-    assert np.array_equal(s1[rows:], stats[rows:])              # rows past `rows` untouched
-    # numpy: out = LN(res) + X W^T + bias; xh = LN'(out)
-    r = (res.astype(np.float64) - mean[:, None]) * stats[:, 1:2] * lnw + lnb
-    ref = r + X.astype(np.float64) @ deq.astype(np.float16).astype(np.float64).T + bias
-    assert np.abs(o1 - ref).max() <= 2e-3 * np.abs(ref).max()
-    xref, mref, sref = ln_ref(o1[:rows].astype(np.float64), nw, nb)
-    assert np.abs(x1[:rows] - xref).max() <= 4e-3 * np.abs(xref).max()
-    assert np.allclose(s1[:rows, 0], mref, rtol=1e-4, atol=1e-4)
-    assert np.allclose(s1[:rows, 1], sref, rtol=1e-4)
+    y = rng.standard_normal((M, N)) * 2 + 0.5
+    g, be, gn = (rng.standard_normal(N).astype(np.float32) * s + o for s, o in ((0.3, 1.0), (0.1, 0.0), (0.3, 1.0)))
+    gn[11] = 0.3
+    mean, r = ln_ref(y)
+    stats = np.ascontiguousarray(np.stack([mean, r], axis=1), np.float32)
+    z = np.ascontiguousarray((y * g).astype(np.float16))
+    out = np.zeros((M, N), np.float16)
+    st = np.zeros((M, 2), np.float32)
+    rc = lib.bertx_test_gemm_ln(fmt, N, K, wb, f32p(bias), M, X.ctypes.data, None, None, None, 2, z.ctypes.data,
+                                stats.ctypes.data, f32p(g), f32p(be), f32p(gn), out.ctypes.data, st.ctypes.data, cfg)
+    assert rc == 0
+    resid = r[:, None] * z.astype(np.float64) - (r * mean)[:, None] * g + be
+    y2 = resid + X.astype(np.float64) @ deq.astype(np.float16).astype(np.float64).T + bias
+    ref = y2 * gn
+    assert np.abs(out - ref).max() <= 2e-3 * np.abs(ref).max()
+    m2, r2 = ln_ref(y2)
+    assert np.allclose(st[:, 0], m2, rtol=1e-4, atol=1e-5 * np.abs(y2).max())
+    assert np.allclose(st[:, 1], r2, rtol=2e-4)
+    # plain residual (no LN on it, no statistics): f16(res + x W^T + b)
+    out2 = np.zeros((M, N), np.float16)
+    rc = lib.bertx_test_gemm_ln(fmt, N, K, wb, f32p(bias), M, X.ctypes.data, None, None, None, 2, z.ctypes.data,
+                                None, None, None, None, out2.ctypes.data, None, cfg)
+    assert rc == 0
+    ref2 = z.astype(np.float64) + X.astype(np.float64) @ deq.astype(np.float16).astype(np.float64).T + bias
+    assert np.abs(out2 - ref2).max() <= 2e-3 * np.abs(ref2).max()
 
 
 def attention_ref(qkv, cu, n_head, d):
@@ -182,11 +198,10 @@ def attention_ref(qkv, cu, n_head, d):
     return out
 
 
-@pytest.mark.parametrize("variant,dh", [(0, 64), (7, 64), (8, 64), (1, 64), (2, 64), (6, 64), (-1, 64), (0, 32),
-                                        (-1, 32)])
+@pytest.mark.parametrize("variant,dh", [(0, 64), (7, 64), (-1, 64), (0, 32), (-1, 32)])
 def test_attention_matches_numpy(lib, variant, dh):
     """Ragged sentences (1 .. 512 tokens, block edges), one with sharp scores whose row
-    maximum moves late (exercises the deferred-max rescale of variant 2)."""
+    maximum moves late (exercises the production kernel's offset move + rescale)."""
     n_head = 4
     d = n_head * dh
     lens = [1, 5, 63, 64, 65, 200, 512, 130]
