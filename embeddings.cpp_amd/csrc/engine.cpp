@@ -480,7 +480,7 @@ int Device::launch_all(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, in
                        hipStream_t s, bool check)
 {
     const int d = hp_.n_embd, f = hp_.n_intermediate;
-    const int M = (int)align_up((size_t)T, GEMM_BM);
+    const int M = gemm_rows(T);   // GEMM rows: T padded to whole tiles
     const double t = (double)T;
     hipEvent_t ev;
     unsigned *cnt = nullptr;
@@ -763,7 +763,10 @@ extern "C" int32_t bertx_bench_gemm(int32_t fmt, int32_t N, int32_t K, int32_t M
     const float *dbias = (const float *)B.up(hb.data(), hb.size() * 4, 0);
     void *dx = B.up(hx.data(), hx.size() * 2, 0);
     void *dout = B.up(nullptr, 0, (size_t)Mp * N * 2);
-    if (epi == EPI_BIAS_RES) {
+    const bool plain = cfg & 0x100;   // A/B: the same GEMM without the LN fold
+    cfg &= 0xff;
+    if (plain) {
+    } else if (epi == EPI_BIAS_RES) {
         ln.res_stats = (const float2 *)B.up(hs.data(), hs.size() * 4, 0);
         ln.res_g = (const float *)B.up(hg.data(), (size_t)N * 4, 0);
         ln.res_b = (const float *)B.up(hbt.data(), (size_t)N * 4, 0);

@@ -17,7 +17,9 @@
 // swizzle on the source address (chunk c ^ ((row>>1)&7)), which keeps the
 // B-operand row read (ds_read_b128, lanes = 16 rows x 4 chunks) conflict-free.
 //   NW 4, BM 256, NS 2 / BM 128, NS 4: two workgroups per CU (64 KiB each), so
-//   one's epilogue overlaps the other's MFMAs.
+//   one's epilogue overlaps the other's MFMAs;
+//   NW 2, BM 64, NS 4 (64 x 64 tiles, 32 KiB): small batches, where the larger
+//   tiles would leave CUs idle.
 // Epilogue: accumulator pairs of adjacent 16-token groups are exchanged with
 // v_permlane16_swap so each lane owns 8 consecutive features of one token
 // (16-B loads of bias / residual / LN parameters and one 16-B store); the
@@ -92,7 +94,7 @@ __device__ __forceinline__ void zmma_items(const R &cur, uint32_t b0, uint32_t b
 
 // The tile body: workgroup b of a grid of nTiles tiles (nN column tiles),
 // staging X in `smem` (NS * BM * 128 B of LDS).
-template <int FMT, int EPI, int NW, int BM, int NS>
+template <int FMT, int EPI, bool LNF, int NW, int BM, int NS>
 __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b, DevWeight W,
                                            const h16 *__restrict__ X, const float *__restrict__ bias,
                                            const void *__restrict__ res, void *__restrict__ out, int nN, int nTiles,
@@ -234,9 +236,9 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     f32x4 bb[2][2];
     col8(bias, bb);
     constexpr bool RES = EPI == EPI_BIAS_RES;
-    const bool lni = !RES && ln.in_stats;       // input LayerNorm folded (wave-uniform)
-    const bool rln = RES && ln.res_stats;       // residual given as z = y * gamma of an LN
-    const bool nxt = RES && ln.g_next;          // emit z' = y' * g_next and partial statistics
+    constexpr bool lni = !RES && LNF;           // input LayerNorm folded
+    constexpr bool rln = RES && LNF;            // residual given as z = y * gamma of an LN ...
+    constexpr bool nxt = RES && LNF;            // ... and z' = y' * g_next + partial statistics out
     f32x4 c1[2][2], rg[2][2], gn[2][2];
     if (lni) col8(ln.c1, c1);
     if (rln) {
@@ -249,7 +251,7 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     }
     if (nxt) col8(ln.g_next, gn);
     const float2 *stp = RES ? ln.res_stats : ln.in_stats;
-    const bool use_st = RES ? rln : lni;
+    constexpr bool use_st = LNF;
     // every residual row chunk and LN statistic of up to 8 token pairs in flight
     // before the first use (one latency, not one per pair)
     constexpr int JC = NJ < 16 ? NJ : 8;        // token groups per prefetch chunk
@@ -260,7 +262,8 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
 #pragma unroll
         for (int jp = 0; jp < JC / 2; ++jp) {
             const int tok = m0 + 16 * (jc + 2 * jp + (g & 1)) + fr;
-            sts[jp] = use_st ? stp[tok] : float2{0.f, 1.f};
+            if constexpr (use_st) sts[jp] = stp[tok];
+            else sts[jp] = float2{0.f, 1.f};
             if constexpr (RES) {
 #pragma unroll
                 for (int a = 0; a < 2; ++a)
@@ -343,56 +346,62 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     }
 }
 
-template <int FMT, int EPI, int NW, int BM, int NS>
-__global__ __launch_bounds__(64 * NW, 8 / NW) void gemmz_kernel(DevWeight W, const h16 *__restrict__ X,
+template <int FMT, int EPI, bool LNF, int NW, int BM, int NS>
+__global__ __launch_bounds__(64 * NW, 2) void gemmz_kernel(DevWeight W, const h16 *__restrict__ X,
                                                                const float *__restrict__ bias,
                                                                const void *__restrict__ res, void *__restrict__ out,
                                                                int nN, int nTiles, LnFold ln)
 {
     __shared__ __attribute__((aligned(16))) char smem[NS * BM * ZK * 2];
-    gemmz_body<FMT, EPI, NW, BM, NS>(smem, blockIdx.x, W, X, bias, res, out, nN, nTiles, ln);
+    gemmz_body<FMT, EPI, LNF, NW, BM, NS>(smem, blockIdx.x, W, X, bias, res, out, nN, nTiles, ln);
 }
 
 template <int FMT, int NW, int BM, int NS>
 void dispatch_z(const DevWeight &W, const h16 *x, int M, const float *bias, int epi, const void *res, void *out,
-                hipStream_t s, const LnFold &ln)
+                hipStream_t s, const LnFold &ln, bool lnf)
 {
     constexpr int BN = 32 * NW;
     const int nN = (W.N + BN - 1) / BN, nTiles = (M / BM) * nN;
-    if (epi == EPI_BIAS_F16)
-        gemmz_kernel<FMT, EPI_BIAS_F16, NW, BM, NS><<<nTiles, 64 * NW, 0, s>>>(W, x, bias, res, out, nN, nTiles, ln);
-    else if (epi == EPI_BIAS_GELU_F16)
-        gemmz_kernel<FMT, EPI_BIAS_GELU_F16, NW, BM, NS><<<nTiles, 64 * NW, 0, s>>>(W, x, bias, res, out, nN, nTiles,
-                                                                                   ln);
-    else
-        gemmz_kernel<FMT, EPI_BIAS_RES, NW, BM, NS><<<nTiles, 64 * NW, 0, s>>>(W, x, bias, res, out, nN, nTiles, ln);
+    auto go = [&](auto kern) { kern<<<nTiles, 64 * NW, 0, s>>>(W, x, bias, res, out, nN, nTiles, ln); };
+    if (epi == EPI_BIAS_F16) {
+        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_F16, true, NW, BM, NS>);
+        else go(gemmz_kernel<FMT, EPI_BIAS_F16, false, NW, BM, NS>);
+    } else if (epi == EPI_BIAS_GELU_F16) {
+        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_GELU_F16, true, NW, BM, NS>);
+        else go(gemmz_kernel<FMT, EPI_BIAS_GELU_F16, false, NW, BM, NS>);
+    } else {
+        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_RES, true, NW, BM, NS>);
+        else go(gemmz_kernel<FMT, EPI_BIAS_RES, false, NW, BM, NS>);
+    }
 }
 
-// Co-resident 4-wave workgroups the device holds at once (two per CU).
-int z_slots()
+// CUs of the current device.
+int z_cus()
 {
-    static const int slots = [] {
-        int dev = 0, cus = 0;
+    static const int cus = [] {
+        int dev = 0, n = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-            cus = 256;
-        return 2 * cus;
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+        return n;
     }();
-    return slots;
+    return cus;
 }
 
 template <int FMT>
 void launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, int32_t epi, const void *res,
-                void *out, hipStream_t s, const LnFold &ln, int cfg)
+                void *out, hipStream_t s, const LnFold &ln, bool lnf, int cfg)
 {
     if (cfg == 0) {
-        // measured in the forward at C3 (profiles/r01_gemm16_sweep.log): 256 x 128
-        // tiles two per CU beat 128 x 128 once there are two such tiles per CU
-        const bool fills = M % 256 == 0 && (long)(M / 256) * (W.N / 128) >= z_slots();
-        cfg = fills ? 2 : 3;
+        // the largest tile that still gives every CU work: 256 x 128 tiles two per CU
+        // (measured fastest at C3 once there are two per CU, profiles/r01_gemm16_sweep.log),
+        // else 128 x 128 once there is one per CU, else 64 x 64 (small batches)
+        const long n128 = (W.N + 127) / 128, cus = z_cus();
+        cfg = (M % 256 == 0 && (M / 256) * n128 >= 2 * cus) ? 2 : (M % 128 == 0 && (M / 128) * n128 >= cus) ? 3 : 4;
     }
-    if (cfg == 2 && M % 256 == 0) dispatch_z<FMT, 4, 256, 2>(W, x, M, bias, epi, res, out, s, ln);
-    else dispatch_z<FMT, 4, 128, 4>(W, x, M, bias, epi, res, out, s, ln);
+    if (cfg == 2 && M % 256 == 0) dispatch_z<FMT, 4, 256, 2>(W, x, M, bias, epi, res, out, s, ln, lnf);
+    else if (cfg != 4 && M % 128 == 0) dispatch_z<FMT, 4, 128, 4>(W, x, M, bias, epi, res, out, s, ln, lnf);
+    else dispatch_z<FMT, 2, 64, 4>(W, x, M, bias, epi, res, out, s, ln, lnf);
 }
 
 }  // namespace
@@ -403,13 +412,19 @@ int launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *b
                 void *out, hipStream_t s, const LnFold &ln)
 {
     const h16 *x = (const h16 *)X;
-    if (W.N % 32 || W.K % ZK || M % 128) return -1;
+    if (W.N % 32 || W.K % ZK || M % 64 || M <= 0) return -1;
+    // the LN fold runs whole or not at all: input (mean, 1/sigma) + c1, or residual
+    // LN + next gamma + partials
+    const bool res_ln = ln.res_stats && ln.res_g && ln.res_b && ln.g_next && ln.part;
+    if (epi == EPI_BIAS_RES && !res_ln && (ln.res_stats || ln.g_next)) return -1;
+    if (epi != EPI_BIAS_RES && ln.in_stats && !ln.c1) return -1;
+    const bool lnf = epi == EPI_BIAS_RES ? res_ln : ln.in_stats != nullptr;
     const int cfg = g_gemm_cfg;
     switch (W.fmt) {
-    case FMT_Q4_0: launch_fmt<FMT_Q4_0>(W, x, M, bias, epi, res, out, s, ln, cfg); break;
-    case FMT_Q4_1: launch_fmt<FMT_Q4_1>(W, x, M, bias, epi, res, out, s, ln, cfg); break;
-    case FMT_Q8_0: launch_fmt<FMT_Q8_0>(W, x, M, bias, epi, res, out, s, ln, cfg); break;
-    default: launch_fmt<FMT_F16>(W, x, M, bias, epi, res, out, s, ln, cfg); break;
+    case FMT_Q4_0: launch_fmt<FMT_Q4_0>(W, x, M, bias, epi, res, out, s, ln, lnf, cfg); break;
+    case FMT_Q4_1: launch_fmt<FMT_Q4_1>(W, x, M, bias, epi, res, out, s, ln, lnf, cfg); break;
+    case FMT_Q8_0: launch_fmt<FMT_Q8_0>(W, x, M, bias, epi, res, out, s, ln, lnf, cfg); break;
+    default: launch_fmt<FMT_F16>(W, x, M, bias, epi, res, out, s, ln, lnf, cfg); break;
     }
     return 0;
 }

@@ -55,7 +55,10 @@ struct DevTable {
 
 enum Epi : int32_t { EPI_BIAS_F16 = 0, EPI_BIAS_GELU_F16 = 1, EPI_BIAS_RES = 2 };
 
-constexpr int GEMM_BM = 256;          // token rows per tile (M is padded to this)
+constexpr int GEMM_BM = 256;          // largest token tile: batches of >= GEMM_PAD_BIG tokens pad to it
+constexpr int GEMM_PAD_BIG = 4096;
+constexpr int GEMM_BM_MIN = 64;       // smaller batches pad to the 64-row tile
+inline int gemm_rows(int T) { const int a = T >= GEMM_PAD_BIG ? GEMM_BM : GEMM_BM_MIN; return (T + a - 1) / a * a; }
 constexpr int ATT_QT = 128;           // queries per attention workgroup (sentences > ATT_LDS_MAX)
 constexpr int ATT_LDS_MAX = 512;      // sentences up to this length: whole K/V of a head in LDS
 
@@ -79,13 +82,14 @@ struct LnFold {
     int32_t part_stride = 0;
 };
 
-// Y[m][n] = epi( sum_k X[m][k] W[n][k] ), X f16 [M][K] with M % 128 == 0 (tiles of
-// 256 or 128 rows: every row of every tile is computed and stored), Y f16 [M][N].
+// Y[m][n] = epi( sum_k X[m][k] W[n][k] ), X f16 [M][K] with M % 64 == 0 (tiles of
+// 256, 128 or 64 rows: every row of every tile is computed and stored), Y f16 [M][N].
 // EPI_BIAS_RES: Y = residual + acc + bias (f32 math), res may alias out (in place,
 // element-wise).  Returns 0, or -1 for an unsupported shape.
 int launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi,
                 const void *res, void *out, hipStream_t s, const LnFold &ln = LnFold());
-// Tests/benches: tile config (0 = heuristic, 2 = 4 waves 256x128, 3 = 4 waves 128x128).
+// Tests/benches: tile config (0 = heuristic, 2 = 4 waves 256x128, 3 = 4 waves 128x128,
+// 4 = 2 waves 64x64).
 extern int g_gemm_cfg;
 
 // z = f16((pos[i] + (type[0] + word[id])) * gamma) and the (mean, 1/sigma) of

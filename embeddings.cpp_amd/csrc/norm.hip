@@ -100,11 +100,14 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(DevTable word, DevTable t
 }
 
 // Row statistics from the residual GEMM's 32-feature group partials (sum, M2 about
-// the group mean): mean = sum / d, M2 = sum_g M2_g + (s_g - 32 mean)^2 / 32 (Chan et al.)
-__global__ __launch_bounds__(256) void ln_stats_kernel(const float2 *__restrict__ part, int G, int stride, int rows,
-                                                       int d, float2 *__restrict__ stats)
+// the group mean): mean = sum / d, M2 = sum_g M2_g + (s_g - 32 mean)^2 / 32 (Chan
+// et al.).  One thread per row, its G partials loaded at once (G <= 32, unrolled:
+// every load in flight before the first add), 64-row blocks so short batches still
+// spread over the CUs; reads part[g][rows] coalesced along the rows.
+__global__ __launch_bounds__(64) void ln_stats_any(const float2 *__restrict__ part, int G, int stride, int rows,
+                                                   int d, float2 *__restrict__ stats)
 {
-    const int t = blockIdx.x * 256 + threadIdx.x;
+    const int t = blockIdx.x * 64 + threadIdx.x;
     if (t >= rows) return;
     float s = 0.f;
     for (int g = 0; g < G; ++g) s += part[(size_t)g * stride + t].x;
@@ -114,6 +117,28 @@ __global__ __launch_bounds__(256) void ln_stats_kernel(const float2 *__restrict_
         const float2 p = part[(size_t)g * stride + t];
         const float dm = p.x - 32.0f * mean;
         m2 += p.y + dm * dm * (1.0f / 32.0f);
+    }
+    stats[t] = float2{mean, 1.0f / sqrtf(m2 / (float)d + 1e-5f)};
+}
+
+template <int G>
+__global__ __launch_bounds__(64) void ln_stats_kernel(const float2 *__restrict__ part, int stride, int rows, int d,
+                                                      float2 *__restrict__ stats)
+{
+    const int t = blockIdx.x * 64 + threadIdx.x;
+    if (t >= rows) return;
+    float2 p[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) p[g] = part[(size_t)g * stride + t];
+    float s = 0.f;
+#pragma unroll
+    for (int g = 0; g < G; ++g) s += p[g].x;
+    const float mean = s / (float)d;
+    float m2 = 0.f;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const float dm = p[g].x - 32.0f * mean;
+        m2 += p[g].y + dm * dm * (1.0f / 32.0f);
     }
     stats[t] = float2{mean, 1.0f / sqrtf(m2 / (float)d + 1e-5f)};
 }
@@ -221,7 +246,18 @@ void launch_embed_ln(const DevTable &word, const DevTable &type, const DevTable 
 void launch_ln_stats(const float2 *part, int32_t G, int32_t stride, int32_t rows, int32_t d, float2 *stats,
                      hipStream_t s)
 {
-    if (rows > 0) ln_stats_kernel<<<(rows + 255) / 256, 256, 0, s>>>(part, G, stride, rows, d, stats);
+    if (rows <= 0) return;
+    const int nb = (rows + 63) / 64;
+    switch (G) {
+    case 12: ln_stats_kernel<12><<<nb, 64, 0, s>>>(part, stride, rows, d, stats); break;   // d 384
+    case 16: ln_stats_kernel<16><<<nb, 64, 0, s>>>(part, stride, rows, d, stats); break;
+    case 24: ln_stats_kernel<24><<<nb, 64, 0, s>>>(part, stride, rows, d, stats); break;   // d 768
+    case 32: ln_stats_kernel<32><<<nb, 64, 0, s>>>(part, stride, rows, d, stats); break;   // d 1024
+    default:
+        // other widths (d % 64 == 0, d <= 1024): the same arithmetic, loads in a loop
+        ln_stats_any<<<nb, 64, 0, s>>>(part, G, stride, rows, d, stats);
+        break;
+    }
 }
 
 int32_t pool_chunks(int32_t max_len) { return (max_len + POOL_CHUNK - 1) / POOL_CHUNK; }

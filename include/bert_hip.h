@@ -71,7 +71,8 @@ BERT_API int32_t bertx_convert_hf(const char *dir_model, const char *fname_out, 
  * in format `fmt` = 0,1,2,3,8).  x: f16 bits [M][K].  epi: 0 = +bias -> f16,
  * 1 = +bias, era GELU -> f16, 2 = +bias +res -> f16 (res f16 [M][N], the
  * residual-stream form; sum in f32, computed in place over res).  cfg: GEMM tile
- * config (0 = the production heuristic, 2 = 4 waves 256x128, 3 = 4 waves 128x128).
+ * config (0 = the production heuristic, 2 = 4 waves 256x128, 3 = 4 waves 128x128,
+ * 4 = 2 waves 64x64).
  * Reference interface these kernels replace: ggml_mul_mat + ggml_add (+ ggml_gelu)
  * at bert.cpp:994-1016, 1040-1045, 1059-1072.
  */
@@ -101,7 +102,8 @@ BERT_API int32_t bertx_test_gemm_ln(int32_t fmt, int32_t N, int32_t K, const voi
  * GEMM micro-benchmark on random operands (device 0): average device time of
  * `iters` launches of the GEMM for fmt / N / K / M / epi / cfg (as
  * bertx_test_gemm), in the forward's own forms: the LN fold on the input of
- * epi 0/1, the residual LN + next gamma + partial statistics for epi 2.
+ * epi 0/1, the residual LN + next gamma + partial statistics for epi 2
+ * (cfg | 0x100: the plain forms, for A/B).
  */
 BERT_API int32_t bertx_bench_gemm(int32_t fmt, int32_t N, int32_t K, int32_t M, int32_t epi, int32_t cfg,
                                   int32_t iters, float *avg_us);
