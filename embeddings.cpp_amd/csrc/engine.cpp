@@ -59,10 +59,47 @@ struct Piece {
     size_t off = 0;
 };
 
+void repack_linear(const std::vector<const HostTensor *> &parts, int fmt_dev, Piece &qs, Piece &dpl, Piece &mpl,
+                   int &N_out, int &K_out);
+
+// f32 weights (ftype 0 files, bert.cpp:499-503): each row w becomes the f16 pair
+// hi = f16(w), lo = f16(w - hi) laid out as ONE f16 row of 2K, [hi | lo]; the GEMM
+// reads X twice along that K (DevWeight::kx), so acc = X W_hi^T + X W_lo^T in f32
+// with the weights good to ~2^-22 instead of f16's 2^-11.
+void repack_linear_f32(const std::vector<const HostTensor *> &parts, Piece &qs, Piece &dpl, Piece &mpl, int &N_out,
+                       int &K_out)
+{
+    const int K = parts[0]->ne0;
+    std::vector<HostTensor> hl(parts.size());
+    std::vector<const HostTensor *> hp;
+    for (size_t i = 0; i < parts.size(); ++i) {
+        const HostTensor &t = *parts[i];
+        HostTensor &o = hl[i];
+        o.fmt = FMT_F16; o.ne0 = 2 * K; o.ne1 = t.ne1;
+        o.bytes.assign((size_t)t.ne1 * 2 * K * 2, 0);
+        std::vector<float> row((size_t)K);
+        for (int r = 0; r < t.ne1; ++r) {
+            dequant_row(t.fmt, t.bytes.data() + fmt_row_bytes(t.fmt, K) * r, row.data(), K);
+            uint16_t *dst = (uint16_t *)o.bytes.data() + (size_t)r * 2 * K;
+            for (int k = 0; k < K; ++k) {
+                const uint16_t h = f32_to_f16(row[(size_t)k]);
+                dst[k] = h;
+                dst[K + k] = f32_to_f16(row[(size_t)k] - f16_to_f32(h));
+            }
+        }
+        hp.push_back(&o);
+    }
+    repack_linear(hp, FMT_F16, qs, dpl, mpl, N_out, K_out);
+}
+
 // Linear weight [N][K] (file rows) -> the lane-order device layout (kernels.h).
 void repack_linear(const std::vector<const HostTensor *> &parts, int fmt_dev, Piece &qs, Piece &dpl, Piece &mpl,
                    int &N_out, int &K_out)
 {
+    if (fmt_dev == FMT_F32) {
+        repack_linear_f32(parts, qs, dpl, mpl, N_out, K_out);
+        return;
+    }
     const int K = parts[0]->ne0;
     int N = 0;
     for (const HostTensor *t : parts) N += t->ne1;
@@ -119,9 +156,10 @@ void repack_linear(const std::vector<const HostTensor *> &parts, int fmt_dev, Pi
 // LN fold constants (kernels.h) of a projection W (the concatenated parts) that
 // reads LN(y) = gamma (y - mean) r + beta: c1[n] = sum_k W[n][k] gamma[k],
 // c2[n] = b[n] + sum_k W[n][k] beta[k], with W as the GEMM multiplies it (each
-// weight rounded once to f16 after dequantization), summed in double.
+// weight rounded once to f16 after dequantization, or the f32 value itself for
+// the hi/lo pairs of f32 files), summed in double.
 void fold_ln(const std::vector<const HostTensor *> &parts, const std::vector<const HostTensor *> &bias,
-             const HostTensor &gamma, const HostTensor &beta, Piece &c1, Piece &c2)
+             const HostTensor &gamma, const HostTensor &beta, Piece &c1, Piece &c2, bool exact)
 {
     const int K = parts[0]->ne0;
     const float *gm = (const float *)gamma.bytes.data(), *bt = (const float *)beta.bytes.data();
@@ -132,7 +170,8 @@ void fold_ln(const std::vector<const HostTensor *> &parts, const std::vector<con
             dequant_row(t->fmt, t->bytes.data() + rb * r, row.data(), K);
             double s1 = 0.0, s2 = 0.0;
             for (int k = 0; k < K; ++k) {
-                const double w = (double)f16_to_f32(f32_to_f16(row[(size_t)k]));
+                // the weight as the GEMM multiplies it: f16-rounded, or hi + lo (f32 files)
+                const double w = exact ? (double)row[(size_t)k] : (double)f16_to_f32(f32_to_f16(row[(size_t)k]));
                 s1 += w * gm[k];
                 s2 += w * bt[k];
             }
@@ -225,7 +264,8 @@ void Device::upload(const HostModel &m)
                      d, f, d / hp_.n_head);
         return;
     }
-    wfmt_ = (hp_.ftype == FMT_F32 || hp_.ftype == FMT_F16) ? FMT_F16 : hp_.ftype;
+    // f32 files keep f32-accurate weights as f16 hi/lo pairs (repack_linear_f32)
+    wfmt_ = hp_.ftype;
     std::vector<Piece> pieces;
     pieces.reserve(16 + 24 * (size_t)hp_.n_layer);
     auto add = [&](Piece &&p) -> size_t { pieces.push_back(std::move(p)); return pieces.size() - 1; };
@@ -251,7 +291,7 @@ void Device::upload(const HostModel &m)
     auto fold = [&](std::vector<const HostTensor *> parts, std::vector<const HostTensor *> bias,
                     const HostTensor &gamma, const HostTensor &beta, size_t &i1, size_t &i2) {
         Piece c1, c2;
-        fold_ln(parts, bias, gamma, beta, c1, c2);
+        fold_ln(parts, bias, gamma, beta, c1, c2, wfmt_ == FMT_F32);
         i1 = add(std::move(c1));
         i2 = add(std::move(c2));
     };
@@ -299,7 +339,8 @@ void Device::upload(const HostModel &m)
     ln_e_b_ = (float *)P(lnb);
     auto mk_lin = [&](const LinIdx &x) {
         DevWeight w;
-        w.fmt = wfmt_; w.N = x.N; w.K = x.K;
+        w.fmt = wfmt_ == FMT_F32 ? FMT_F16 : wfmt_; w.N = x.N; w.K = x.K;
+        w.kx = wfmt_ == FMT_F32 ? x.K / 2 : 0;
         w.qs = P(x.q); w.d = (const uint16_t *)P(x.d); w.m = (const uint16_t *)P(x.m);
         return w;
     };
@@ -634,10 +675,10 @@ bool hook_weight(int32_t fmt, int32_t N, int32_t K, const void *w_rows, HostTens
 {
     t.fmt = fmt; t.ne0 = K; t.ne1 = N;
     t.bytes.assign((const uint8_t *)w_rows, (const uint8_t *)w_rows + fmt_row_bytes(fmt, K) * (size_t)N);
-    const int fdev = (fmt == FMT_F32 || fmt == FMT_F16) ? FMT_F16 : fmt;
     Piece q, dd, mm;
-    repack_linear({&t}, fdev, q, dd, mm, W.N, W.K);
-    W.fmt = fdev;
+    repack_linear({&t}, fmt, q, dd, mm, W.N, W.K);
+    W.fmt = fmt == FMT_F32 ? FMT_F16 : fmt;
+    W.kx = fmt == FMT_F32 ? W.K / 2 : 0;
     W.qs = B.up(q.bytes.data(), q.bytes.size(), 0);
     W.d = (const uint16_t *)(dd.bytes.empty() ? nullptr : B.up(dd.bytes.data(), dd.bytes.size(), 0));
     W.m = (const uint16_t *)(mm.bytes.empty() ? nullptr : B.up(mm.bytes.data(), mm.bytes.size(), 0));
@@ -687,7 +728,7 @@ extern "C" int32_t bertx_test_gemm_ln(int32_t fmt, int32_t N, int32_t K, const v
         // the LN fold of the input: c1 = W gamma, c2 = bias + W beta
         const HostTensor hb = vec_tensor(bias, N), hg = vec_tensor(in_g, K), hbt = vec_tensor(in_b, K);
         Piece c1, c2;
-        fold_ln({&t}, {&hb}, hg, hbt, c1, c2);
+        fold_ln({&t}, {&hb}, hg, hbt, c1, c2, fmt == FMT_F32);
         ln.in_stats = (const float2 *)B.up(in_stats, (size_t)M * 8, (size_t)Mp * 8);
         ln.c1 = (const float *)B.up(c1.bytes.data(), c1.bytes.size(), 0);
         dbias = (const float *)B.up(c2.bytes.data(), c2.bytes.size(), 0);

@@ -115,6 +115,7 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     const int t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
     const int m0 = (t / nN) * BM, n0 = (t % nN) * BN;
     const int K = W.K, N = W.N, KS = K / ZK;
+    const int KX = W.kx ? W.kx : K, KSX = KX / ZK;   // X columns (f32 hi/lo weights: K = 2 KX)
     const int fr = lane & 15, g = lane >> 4;
     const int nw = n0 + 32 * wave;              // this wave's first feature
     const int grp = min(nw, N - 32) >> 5;       // its 32-feature weight group (clamped past N)
@@ -124,19 +125,20 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     // lane/8; the swizzle ((row>>1)&7) only differs between even and odd i, so
     // one offset VGPR per parity and the row step in soffset
     const __amdgpu_buffer_rsrc_t xrs =
-        __builtin_amdgcn_make_buffer_rsrc((void *)(X + (size_t)m0 * K), (short)0, BM * K * 2, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void *)(X + (size_t)m0 * KX), (short)0, BM * KX * 2, 0x00020000);
     uint32_t xvo[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int r = 8 * XG * wave + 8 * i + (lane >> 3);
-        xvo[i] = (uint32_t)(r * K + (((lane & 7) ^ ((r >> 1) & 7)) * 8)) * 2u;
+        xvo[i] = (uint32_t)(r * KX + (((lane & 7) ^ ((r >> 1) & 7)) * 8)) * 2u;
     }
     auto issue_x = [&](int ks, int stage) {
         char *dst = smem + stage * XB + ((8 * XG * wave) << 7);
+        const int kc = ks < KSX ? ks : ks - KSX;   // the X column block of K-step ks
 #pragma unroll
         for (int i = 0; i < XG; ++i)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_void_t *)(dst + (i << 10)), 16, xvo[i & 1],
-                                                     ((i >> 1) * 16 * K + ks * ZK) * 2, 0, 0);
+                                                     ((i >> 1) * 16 * KX + kc * ZK) * 2, 0, 0);
     };
     const uint8_t *wq = (const uint8_t *)W.qs + ((size_t)grp * 64 + lane) * QB;
     const uint16_t *wd = W.d + ((size_t)grp * 16 + fr) * 4;
@@ -412,7 +414,7 @@ int launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *b
                 void *out, hipStream_t s, const LnFold &ln)
 {
     const h16 *x = (const h16 *)X;
-    if (W.N % 32 || W.K % ZK || M % 64 || M <= 0) return -1;
+    if (W.N % 32 || W.K % ZK || M % 64 || M <= 0 || (W.kx && (W.kx % ZK || 2 * W.kx != W.K))) return -1;
     // the LN fold runs whole or not at all: input (mean, 1/sigma) + c1, or residual
     // LN + next gamma + partials
     const bool res_ln = ln.res_stats && ln.res_g && ln.res_b && ln.g_next && ln.part;

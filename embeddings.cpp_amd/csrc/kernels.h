@@ -8,7 +8,8 @@
 //              q4_0/q4_1: 16 B (word u, element i at bit 4(i/2) + 16(i%2), so
 //                    a mask and an OR with the f16 magic 0x6400 give an f16 pair)
 //              q8_0: 32 B (8 B per u, (q ^ 0x80) in order e0 e2 e1 e3 per 4-group)
-//              f16:  64 B (f32 files are rounded to f16)
+//              f16:  64 B; f32 files as f16 (hi, lo) pairs along a doubled K
+//                    (hi = f16(w), lo = f16(w - hi)), X read twice
 //            d (and m) f16 [ks][grp][f][u].  N % 32 == 0, K % 64 == 0.
 //   QKV      the three projections are one [3d][d] weight (one GEMM, N = 3d)
 //   tables   word/type/pos embeddings in the file's format; q blocks split
@@ -38,8 +39,10 @@
 namespace emb {
 
 struct DevWeight {
-    int32_t fmt = 0;   // FMT_F16 (also used for f32 files), FMT_Q4_0, FMT_Q4_1, FMT_Q8_0
+    int32_t fmt = 0;   // FMT_F16, FMT_Q4_0, FMT_Q4_1, FMT_Q8_0
     int32_t N = 0, K = 0;
+    int32_t kx = 0;    // 0: X has K columns; else X has kx = K/2 columns, read twice
+                       // (f32 files: [hi | lo] f16 weight rows, engine.cpp)
     const void *qs = nullptr;       // values / nibbles / int8, lane order
     const uint16_t *d = nullptr;    // f16 scales
     const uint16_t *m = nullptr;    // f16 mins (q4_1)

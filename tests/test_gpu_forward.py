@@ -46,6 +46,22 @@ def test_forward_matches_oracle(quant_models, tiny, fmt):
 
 
 @pytest.mark.parametrize("tiny", ["tiny32", "tiny64"])
+def test_f32_weights_as_tight_as_f16(quant_models, tiny):
+    """f32 files run with f32-accurate weights (f16 hi/lo pairs, engine.cpp repack_linear_f32),
+    not rounded to f16: the f32 model's distance to the oracle's f32 forward (bert.cpp:499-503,
+    f32 x f32) is at most the f16 model's distance to the oracle's f16 forward."""
+    dev = {}
+    for fmt in ("f32", "f16"):
+        path = quant_models[(tiny, fmt)]
+        m = bertpy.BertModel(path)
+        o = oracle_lib.Oracle(path)
+        ids = ragged_ids(o.n_vocab, [2, 3, 17, 64, 100, m.n_max_tokens - 1, m.n_max_tokens, 33])
+        dev[fmt] = float(1.0 - cosines(m.forward_batch(ids), o.forward_batch(ids)).min())
+    print("1 - min cosine vs oracle:", dev)
+    assert dev["f32"] <= max(dev["f16"], 2e-7), dev
+
+
+@pytest.mark.parametrize("tiny", ["tiny32", "tiny64"])
 def test_forward_matches_torch_golden(tiny):
     path = os.path.join(GOLDEN, tiny, "ggml-model-f32.bin")
     g = np.load(os.path.join(GOLDEN, tiny, "forward_f32.npz"))
