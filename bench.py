@@ -42,6 +42,14 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-profile", action="store_true", help="disable live per-kernel event timing")
     p.add_argument("--no-probes", action="store_true", help="skip the north-star probes (C2 f16, B=1 L=32 q4_0)")
+    p.add_argument("--no-library", action="store_true", help="skip the host-buffer library-path measurement")
+    p.add_argument("--inproc", action="store_true",
+                   help="one process drives --gpus GPUs through bert_forward_batch (the library's own sharding, "
+                        "BERT_DEVICES=0..N-1) on --inproc-batch sentences of the --inproc-arch/--inproc-ftype model "
+                        "(default SURVEY C4: bge-large-en-v1.5 q4_1, L 512, 256 sentences)")
+    p.add_argument("--inproc-arch", default="bge-large-en-v1.5")
+    p.add_argument("--inproc-ftype", default="q4_1")
+    p.add_argument("--inproc-batch", type=int, default=256)
     return p.parse_args()
 
 
@@ -208,6 +216,55 @@ def probes(lib, bertpy, torch, a, dev, stream, q4_path):
     return out
 
 
+def library_path(model, ids_list, steps, dist, red_dev):
+    """The reference Python client's path (examples/sample_dylib.py -> bert_forward_batch):
+    host int32 token arrays in, host float32 rows out -- staging copy, H2D, forward,
+    D2H and the copy into the caller's rows all inside the timed region; synchronous
+    calls, K of them between barriers, max over ranks."""
+    for _ in range(2):
+        model.forward_batch(ids_list)
+    el = timed_steps(lambda: model.forward_batch(ids_list), steps, lambda: None, dist, red_dev)
+    return el
+
+
+def run_inproc(a):
+    """--inproc: ONE process drives a.gpus GPUs through the library's own multi-GPU
+    path (bert_abi.cpp run_forward: sentences split over the context's GPUs by FLOP
+    cost, one host thread + stream + weight replica per GPU, no collectives) -- what
+    ctypes and server callers get from bert_forward_batch.  Prints one JSON line."""
+    if "BERT_DEVICES" not in os.environ:
+        os.environ["BERT_DEVICES"] = ",".join(str(i) for i in range(a.gpus))
+    import numpy as np
+    import bertpy
+    hp = bertpy.ARCHS[a.inproc_arch]
+    path = ensure_model(bertpy, a.model_dir, a.inproc_arch, a.inproc_ftype, a.seed)
+    m = bertpy.BertModel(path)
+    nd = m.lib.bertx_num_devices(m.ctx)
+    ids = bertpy.synthetic_ids(a.inproc_batch, a.seq, hp["n_vocab"], seed=7)
+    for _ in range(max(a.warmup, 1)):
+        e = m.forward_batch(ids)
+    assert np.all(np.isfinite(e)) and np.allclose(np.linalg.norm(e, axis=1), 1.0, atol=1e-3)
+    el = timed_steps(lambda: m.forward_batch(ids), a.steps, lambda: None)
+    per = m.device_last_call()
+    busy = [p[0] for p in per if p[1] > 0]
+    flop = a.inproc_batch * flop_per_sentence(hp, a.seq)
+    res = {"metric": f"sentences/sec, {a.inproc_arch} {a.inproc_ftype} seq{a.seq} batch{a.inproc_batch}, "
+                     "library path (bert_forward_batch, host buffers, in-process multi-GPU)",
+           "value": round(a.inproc_batch * a.steps / el, 2), "unit": "sentences/s", "n_gpus": nd,
+           "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 3),
+           "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f16",
+           "data": "synthetic (random-init weights, seeded token ids)",
+           "config": {"workload": f"{a.inproc_arch} {a.inproc_ftype} seq_len {a.seq}, {a.inproc_batch} sentences "
+                                  f"split over {nd} GPU replicas by bert_forward_batch",
+                      "global_batch": a.inproc_batch, "seq_len": a.seq, "weights": a.inproc_ftype,
+                      "devices": os.environ["BERT_DEVICES"], "parallelism": f"in-process replicas x{nd}"},
+           "tflops": round(flop * a.steps / el / 1e12, 1),
+           "per_device_last_call": [{"slot": i, "wall_ms": round(p[0], 3), "sentences": p[1], "tokens": p[2]}
+                                    for i, p in enumerate(per)],
+           "balance_max_over_min_wall": round(max(busy) / min(busy), 3) if busy else None}
+    print(json.dumps(res), flush=True)
+
+
 def flop_per_sentence(hp, L):
     d, f, nl = hp["n_embd"], hp["n_intermediate"], hp["n_layer"]
     return nl * (2 * L * (4 * d * d + 2 * d * f) + 4 * L * L * d)
@@ -216,6 +273,10 @@ def flop_per_sentence(hp, L):
 def main():
     a = parse()
     rank, world, local = dist_env()
+    if a.inproc:
+        assert world == 1, "--inproc runs in one process"
+        run_inproc(a)
+        return
     os.environ["BERT_DEVICES"] = str(local)
     import numpy as np
     import torch
@@ -271,6 +332,9 @@ def main():
 
     ms_per_step = elapsed / a.steps * 1e3
     value = B * world * a.steps / elapsed
+    lib_el = None
+    if not a.no_library:
+        lib_el = library_path(model, ids_list, a.steps, dist, red_dev)
 
     roofline = None
     kernels = {}
@@ -326,6 +390,29 @@ def main():
         "roofline": roofline,
         "kernels": kernels,
     }
+    # measured HBM traffic of the step: per-launch FETCH/WRITE bytes of each kernel
+    # class (rocprofv3 PMC passes of this bench, profiles/pmc_traffic.json) x launches
+    # per step, over the graph-replayed step time
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if stats and os.path.exists(pmc) and not (a.arch != "bge-base-en-v1.5" or a.ftype != "q4_0" or B != 64 or L != 512):
+        try:
+            with open(pmc) as f:
+                tr = json.load(f)
+            per_step = sum(tr[s_["name"]] * s_["launches"] / a.steps for s_ in stats
+                           if s_["launches"] and s_["name"] in tr)
+            res["hbm"] = {"bytes_per_step": int(per_step), "gbps": round(per_step / (ms_per_step * 1e-3) / 1e9, 1),
+                          "peak_gbps": HBM_PEAK_GBPS,
+                          "frac": round(per_step / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                          "source": "profiles/pmc_traffic.json (2 x FETCH_SIZE + WRITE_SIZE per launch, "
+                                    "MI355X_MICROARCH.md gfx950 correction) x launches per step / step time"}
+        except Exception as ex:   # a report, never the metric
+            res["hbm"] = {"error": str(ex)}
+    if lib_el is not None:
+        res["library_path"] = {"value": round(B * world * a.steps / lib_el, 2), "unit": "sentences/s",
+                               "ms_per_step": round(lib_el / a.steps * 1e3, 4),
+                               "workload": "the same batch per GPU through bert_forward_batch from host int32 "
+                                           "arrays into host float rows (the ctypes client's path: staging, "
+                                           "H2D, forward, D2H inside the timed region), one context per rank"}
 
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         try:

@@ -69,6 +69,9 @@ def load_lib(path=None):
     L.bertx_kernel_stats.restype = c_i32
     L.bertx_kernel_stats.argtypes = [vp, c_i32, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_int64),
                                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), c_i32p]
+    L.bertx_device_last_call.restype = c_i32
+    L.bertx_device_last_call.argtypes = [vp, c_i32, ctypes.POINTER(ctypes.c_double), c_i32p,
+                                         ctypes.POINTER(ctypes.c_int64)]
     L.bertx_quantize_file.restype = c_i32
     L.bertx_quantize_file.argtypes = [ctypes.c_char_p, ctypes.c_char_p, c_i32]
     L.bertx_convert_hf.restype = c_i32
@@ -157,6 +160,15 @@ class BertModel:
         a = np.ascontiguousarray(np.asarray(ids, np.int32))
         out = np.zeros(self.n_embd, np.float32)
         self.lib.bert_forward(self.ctx, self.N_THREADS, _as_i32p(a), len(a), _as_f32p(out))
+        return out
+
+    def device_last_call(self):
+        """Per GPU of the context: (wall ms, sentences, tokens) of the last host-driven call."""
+        out = []
+        for i in range(self.lib.bertx_num_devices(self.ctx)):
+            ms, ns, nt = ctypes.c_double(), c_i32(), ctypes.c_int64()
+            self.lib.bertx_device_last_call(self.ctx, i, ctypes.byref(ms), ctypes.byref(ns), ctypes.byref(nt))
+            out.append((ms.value, ns.value, nt.value))
         return out
 
     def hparams(self):

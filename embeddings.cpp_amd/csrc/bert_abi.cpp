@@ -92,6 +92,16 @@ int run_forward(bert_ctx *ctx, const int32_t *const *toks, const int32_t *lens, 
         Device &D = *ctx->devices[(size_t)dv];
         std::lock_guard<std::mutex> lk(D.mutex());
         const std::vector<int> &mine = assign[(size_t)dv];
+        const auto t0 = std::chrono::steady_clock::now();
+        int64_t toks_done = 0;
+        struct Stamp {   // this call's share of the device: wall time, sentences, tokens
+            Device &D; const std::chrono::steady_clock::time_point &t0; const std::vector<int> &mine; int64_t &toks;
+            ~Stamp()
+            {
+                const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+                D.set_last_call(ms, (int)mine.size(), toks);
+            }
+        } stamp{D, t0, mine, toks_done};
         std::vector<const int32_t *> tp;
         std::vector<int32_t> lp;
         std::vector<float *> op;
@@ -107,6 +117,7 @@ int run_forward(bert_ctx *ctx, const int32_t *const *toks, const int32_t *lens, 
             }
             const int rc = D.forward_host(tp.data(), lp.data(), (int)tp.size(), op.data());
             if (rc != 0) { rcs[(size_t)dv] = rc; return; }
+            toks_done += tok;
         }
     };
     int used = 0;
@@ -118,6 +129,8 @@ int run_forward(bert_ctx *ctx, const int32_t *const *toks, const int32_t *lens, 
         for (int dv = 0; dv < nd; ++dv) if (!assign[(size_t)dv].empty()) th.emplace_back(work, dv);
         for (auto &t : th) t.join();
     }
+    for (int dv = 0; dv < nd; ++dv)
+        if (assign[(size_t)dv].empty()) ctx->devices[(size_t)dv]->set_last_call(0.0, 0, 0);
     for (int rc : rcs) if (rc != 0) {
         std::fprintf(stderr, "libbert: forward failed (%d)\n", rc);
         return rc;
@@ -383,6 +396,17 @@ int32_t bertx_kernel_stats(struct bert_ctx *ctx, int32_t idx, const char **name,
     if (work) *work = w;
     if (work_is_flops)
         *work_is_flops = (idx == emb::K_EMBED_LN || idx == emb::K_LN_STATS || idx == emb::K_POOL_L2) ? 0 : 1;
+    return 0;
+}
+
+int32_t bertx_device_last_call(struct bert_ctx *ctx, int32_t slot, double *wall_ms, int32_t *n_seqs,
+                               int64_t *n_tokens)
+{
+    if (!ctx || slot < 0 || slot >= (int32_t)ctx->devices.size()) return -1;
+    const Device &D = *ctx->devices[(size_t)slot];
+    if (wall_ms) *wall_ms = D.last_call_ms();
+    if (n_seqs) *n_seqs = D.last_call_seqs();
+    if (n_tokens) *n_tokens = D.last_call_tokens();
     return 0;
 }
 

@@ -96,6 +96,13 @@ public:
 
     const HParams &hp() const { return hp_; }
 
+    // the last bert_forward_batch / bert_encode_batch call's share of this replica
+    // (bertx_device_last_call): host wall time of its forwards, sentences, tokens
+    void set_last_call(double ms, int seqs, int64_t tokens) { lc_ms_ = ms; lc_seqs_ = seqs; lc_tokens_ = tokens; }
+    double last_call_ms() const { return lc_ms_; }
+    int last_call_seqs() const { return lc_seqs_; }
+    int64_t last_call_tokens() const { return lc_tokens_; }
+
 private:
     struct PendingEv { int cls; hipEvent_t a, b; double work; };
     struct GraphKey {
@@ -159,6 +166,10 @@ private:
     bool use_graphs_ = true;
 
     // profiling
+    double lc_ms_ = 0.0;
+    int lc_seqs_ = 0;
+    int64_t lc_tokens_ = 0;
+
     bool profiling_ = false;
     double att_flop_ = 0.0;         // attention FLOP of the forward being launched
     std::vector<PendingEv> pending_;

@@ -54,6 +54,16 @@ BERT_API int32_t bertx_kernel_stats(struct bert_ctx *ctx, int32_t idx, const cha
                                     int64_t *launches, double *total_ms, double *work,
                                     int32_t *work_is_flops);
 
+/*
+ * Multi-GPU balance of the last host-driven call (bert_forward_batch /
+ * bert_encode_batch, which shard sentences over the context's GPUs by FLOP cost,
+ * reference entry point bert.cpp:1374-1444): GPU `slot`'s host wall time for its
+ * share (staging, H2D, forward, D2H), its sentence and token counts.  Returns 0,
+ * or -1 for a bad slot.
+ */
+BERT_API int32_t bertx_device_last_call(struct bert_ctx *ctx, int32_t slot, double *wall_ms, int32_t *n_seqs,
+                                        int64_t *n_tokens);
+
 /* Native quantizer (mirrors models/quantize.cpp): f32/f16 file -> itype
  * 2 (q4_0), 3 (q4_1) or 8 (q8_0, extension).  Returns 0 on success. */
 BERT_API int32_t bertx_quantize_file(const char *fname_in, const char *fname_out, int32_t itype);

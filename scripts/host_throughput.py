@@ -1,0 +1,239 @@
+#!/usr/bin/env python3
+"""Host-side throughput of the two SURVEY §8(f) rows around the GPU forward.
+
+  tok     (f2, CPU only) WordPiece tokenization of ~508-token texts: the reference's
+          own tokenizer source (bert.cpp:195-417 compiled into oracle/_ref/libreftok.so
+          by oracle/build_ref.sh -- std::map substring probes, one thread, as
+          bert_encode_batch runs it, bert.cpp:1402-1406) against libbert's trie
+          tokenizer (csrc/tokenizer.cpp) on 1 thread and on 8 / 16 threads (ctypes
+          drops the GIL, so Python threads run the C tokenizer in parallel).  Token
+          ids of both are compared on every text.
+  server  (f3, GPU) requests/s of the TCP protocol (examples/server.cpp: int32 n_embd
+          on connect, one text per recv, n_embd float32 back) with 1 / 8 / 64
+          concurrent clients: build/bin/server (micro-batching) against the
+          reference's own examples/server.cpp linked to libbert.so
+          (build/ref_clients/server: one client at a time, one text per forward).
+
+Prints one JSON object per measurement.  Vocab: the 692-entry BERT word-piece vocab
+of the committed fixtures (tests/golden/tokenizer_cases.json); server model: the
+bench's synthetic bge-base-en-v1.5 q4_0 (words w<i> are single tokens, so a text
+of k words is exactly k + 2 tokens).
+"""
+import argparse
+import ctypes
+import json
+import os
+import socket
+import struct
+import subprocess
+import sys
+import threading
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "embeddings.cpp_amd"))
+import bertpy  # noqa: E402
+
+
+def emit(**kw):
+    print(json.dumps(kw), flush=True)
+
+
+def make_texts(vocab, n, n_words, seed=0):
+    """Words of 1-3 word pieces (first piece a whole-word token, later pieces '##'
+    continuations with the '##' dropped), so greedy longest-prefix matching splits
+    them again; some punctuation and accented letters."""
+    rng = np.random.default_rng(seed)
+    whole = [v for v in vocab if v.isalpha() and not v.startswith("[")]
+    subs = [v[2:] for v in vocab if v.startswith("##") and v[2:].isalpha()]
+    extras = [",", ".", "!", "café", "naïve", "(", ")"]
+    out = []
+    for _ in range(n):
+        words = []
+        for _ in range(n_words):
+            r = rng.random()
+            if r < 0.06:
+                words.append(extras[int(rng.integers(len(extras)))])
+                continue
+            w = whole[int(rng.integers(len(whole)))]
+            for _ in range(int(rng.integers(0, 3))):
+                w += subs[int(rng.integers(len(subs)))]
+            words.append(w.upper() if rng.random() < 0.05 else w)
+        out.append(" ".join(words).encode())
+    return out
+
+
+def cmd_tok(a):
+    vocab = json.load(open(os.path.join(ROOT, "tests", "golden", "tokenizer_cases.json")))["vocab"]
+    n_max = 512
+    # size the texts to ~508 tokens with the library tokenizer itself
+    os.environ["BERT_HOST_ONLY"] = "1"
+    lib = bertpy.load_lib()
+    m = bertpy.BertModel(os.path.join(ROOT, "tests", "golden", "tiny32", "ggml-model-f32.bin"), lib=lib)
+    probe = make_texts(vocab, 4, 200, seed=1)
+    per_word = np.mean([m.tokenize(t, 100000)[1] for t in probe]) / 200
+    texts = make_texts(vocab, a.texts, int(506 / per_word), seed=2)
+    cap = 4 * n_max
+    buf = (ctypes.c_int32 * cap)()
+    n = ctypes.c_int32()
+
+    def ours(t, bb, nn):
+        lib.bert_tokenize(m.ctx, t, bb, ctypes.byref(nn), n_max)
+        return nn.value
+
+    lens = [ours(t, buf, n) for t in texts]
+    emit(kind="texts", n=len(texts), mean_tokens=float(np.mean(lens)), min_tokens=int(min(lens)),
+         max_tokens=int(max(lens)))
+
+    res = {}
+    ref_path = os.path.join(ROOT, "oracle", "_ref", "libreftok.so")
+    if os.path.exists(ref_path):
+        R = ctypes.CDLL(ref_path)
+        R.reftok_new.restype = ctypes.c_void_p
+        R.reftok_add.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_int]
+        R.reftok_tokenize.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_int32]
+        rc = R.reftok_new()
+        for i, v in enumerate(vocab):
+            b = v.encode()
+            R.reftok_add(rc, b, len(b), i)
+        rbuf = (ctypes.c_int32 * cap)()
+        # ids equal on every text (the written prefix)
+        for t in texts[:200]:
+            ours(t, buf, n)
+            rn = ctypes.c_int32()
+            R.reftok_tokenize(rc, t, rbuf, ctypes.byref(rn), n_max)
+            assert rn.value == n.value and list(rbuf[:min(n.value, n_max)]) == list(buf[:min(n.value, n_max)])
+        t0 = time.perf_counter()
+        for t in texts:
+            rn = ctypes.c_int32()
+            R.reftok_tokenize(rc, t, rbuf, ctypes.byref(rn), n_max)
+        el = time.perf_counter() - t0
+        res["reference"] = len(texts) / el
+        emit(kind="tokenizer", impl="reference bert.cpp:195-417 (std::map)", threads=1, texts_per_s=round(len(texts) / el, 1),
+             us_per_text=round(el / len(texts) * 1e6, 2))
+    for thr in a.threads:
+        chunks = [texts[i::thr] for i in range(thr)]
+
+        def work(ch):
+            bb = (ctypes.c_int32 * cap)()
+            nn = ctypes.c_int32()
+            for t in ch:
+                ours(t, bb, nn)
+
+        ths = [threading.Thread(target=work, args=(c,)) for c in chunks]
+        t0 = time.perf_counter()
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        el = time.perf_counter() - t0
+        res[thr] = len(texts) / el
+        emit(kind="tokenizer", impl="libbert trie (csrc/tokenizer.cpp)", threads=thr,
+             texts_per_s=round(len(texts) / el, 1), us_per_text_per_thread=round(el * thr / len(texts) * 1e6, 2),
+             vs_reference_1thread=round(res[thr] / res["reference"], 2) if "reference" in res else None)
+
+
+def recv_exact(sock, n):
+    b = b""
+    while len(b) < n:
+        c = sock.recv(n - len(b))
+        if not c:
+            raise RuntimeError("closed")
+        b += c
+    return b
+
+
+def run_server_load(exe_args, port, n_clients, per_client, text, env):
+    proc = subprocess.Popen(exe_args, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, env=env)
+    try:
+        for _ in range(1200):
+            try:
+                socket.create_connection(("127.0.0.1", port), timeout=5).close()
+                break
+            except OSError:
+                if proc.poll() is not None:
+                    raise RuntimeError(f"server exited {proc.returncode}")
+                time.sleep(0.1)
+        errors = []
+        lat = []
+
+        def client():
+            try:
+                with socket.create_connection(("127.0.0.1", port), timeout=300) as s:
+                    nd = struct.unpack("i", recv_exact(s, 4))[0]
+                    for _ in range(per_client):
+                        t0 = time.perf_counter()
+                        s.sendall(text)
+                        recv_exact(s, 4 * nd)
+                        lat.append(time.perf_counter() - t0)
+            except Exception as e:  # noqa: BLE001 -- reported
+                errors.append(repr(e))
+
+        ths = [threading.Thread(target=client) for _ in range(n_clients)]
+        t0 = time.perf_counter()
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join(600)
+        el = time.perf_counter() - t0
+        if errors:
+            raise RuntimeError(errors[:3])
+        return n_clients * per_client / el, float(np.median(lat))
+    finally:
+        proc.kill()
+        proc.wait(timeout=30)
+
+
+def cmd_server(a):
+    model_dir = os.environ.get("EMB_MODEL_DIR", "/tmp/emb_models")
+    os.makedirs(model_dir, exist_ok=True)
+    path = os.path.join(model_dir, "bge-base-en-v1.5-q4_0-seed1234.bin")
+    if not os.path.exists(path):
+        bertpy.synthetic_model(path + ".part", "bge-base-en-v1.5", "q4_0", seed=1234)
+        os.replace(path + ".part", path)
+    text = " ".join(f"w{1000 + 37 * i}" for i in range(a.words)).encode()   # a.words + 2 tokens
+    env = dict(os.environ, BERT_DEVICES="0")
+    env.pop("BERT_HOST_ONLY", None)
+    ours = os.path.join(ROOT, "build", "bin", "server")
+    ref = os.path.join(ROOT, "build", "ref_clients", "server")
+    for n_cli in a.clients:
+        per = max(a.min_requests // n_cli, 2)
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        rps, med = run_server_load([ours, "-m", path, "--port", str(port), "--max-batch", "64", "--wait-us",
+                                    str(a.wait_us)], port, n_cli, per, text, env)
+        emit(kind="server", impl="build/bin/server (micro-batching)", clients=n_cli, tokens_per_text=a.words + 2,
+             requests=n_cli * per, requests_per_s=round(rps, 1), median_latency_ms=round(med * 1e3, 3))
+        if os.path.exists(ref) and n_cli <= 8:
+            # the reference server takes one client at a time (backlog 1, serial accept
+            # loop, examples/server.cpp:92-118): concurrent clients queue behind each other
+            with socket.socket() as s:
+                s.bind(("127.0.0.1", 0))
+                port = s.getsockname()[1]
+            rps, med = run_server_load([ref, "-m", path, "--port", str(port)], port, n_cli, per, text, env)
+            emit(kind="server", impl="reference examples/server.cpp on libbert (batch 1 per recv)", clients=n_cli,
+                 tokens_per_text=a.words + 2, requests=n_cli * per, requests_per_s=round(rps, 1),
+                 median_latency_ms=round(med * 1e3, 3))
+
+
+def main():
+    p = argparse.ArgumentParser()
+    sub = p.add_subparsers(dest="cmd", required=True)
+    t = sub.add_parser("tok")
+    t.add_argument("--texts", type=int, default=2000)
+    t.add_argument("--threads", type=int, nargs="+", default=[1, 8, 16])
+    s = sub.add_parser("server")
+    s.add_argument("--clients", type=int, nargs="+", default=[1, 8, 64])
+    s.add_argument("--words", type=int, default=126)
+    s.add_argument("--min-requests", type=int, default=512)
+    s.add_argument("--wait-us", type=int, default=2000)
+    a = p.parse_args()
+    cmd_tok(a) if a.cmd == "tok" else cmd_server(a)
+
+
+if __name__ == "__main__":
+    main()

@@ -49,8 +49,8 @@ def classify(rows):
                 res_i += 1
         elif "attention" in k:
             c = "attention"
-        elif "layernorm_kernel" in k:
-            c = "layernorm"
+        elif "ln_stats" in k:
+            c = "ln_stats"
         elif "embed_ln_kernel" in k:
             c = "embed_ln"
         elif "pool_partial" in k:
