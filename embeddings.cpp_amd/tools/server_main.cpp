@@ -10,9 +10,10 @@
 // The serving model differs.  The reference accepts one client at a time
 // (listen backlog 1) and runs one bert_encode per recv.  Here every connection
 // has its own thread, which tokenizes its text (bert_tokenize, host) and queues
-// it; one batcher thread sends whatever has arrived within --wait-us of the
-// first queued text (at most --max-batch texts) to the GPU as ONE
-// bert_forward_batch.  Per-sentence results do not depend on the batch they ride
+// it; one batcher thread sends the queued texts (at most --max-batch) to the GPU
+// as ONE bert_forward_batch as soon as every connected client has a text queued,
+// or --wait-us after the first one arrived, whichever comes first (so a lone
+// client never waits for a batch that cannot fill).  Per-sentence results do not depend on the batch they ride
 // in (tests/test_gpu_forward.py batch invariance), so every reply equals the
 // single-text result.
 //
@@ -53,6 +54,15 @@ public:
     {
     }
 
+    // connection count: the batch threshold (a batch is full when every
+    // connected client has a text in it)
+    void connected(int delta)
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        clients_ += delta;
+        cv_in_.notify_one();
+    }
+
     // queues r and blocks until r->emb holds its embedding
     void run(Request *r)
     {
@@ -73,9 +83,12 @@ public:
             {
                 std::unique_lock<std::mutex> lk(mu_);
                 cv_in_.wait(lk, [&] { return !queue_.empty(); });
-                // the window opens with the first queued text
-                cv_in_.wait_for(lk, std::chrono::microseconds(wait_us_),
-                                [&] { return (int)queue_.size() >= max_batch_; });
+                // the window opens with the first queued text and closes early once
+                // every connected client has a text queued
+                cv_in_.wait_for(lk, std::chrono::microseconds(wait_us_), [&] {
+                    const int full = clients_ < max_batch_ ? (clients_ > 1 ? clients_ : 1) : max_batch_;
+                    return (int)queue_.size() >= full;
+                });
                 while (!queue_.empty() && (int)batch.size() < max_batch_) {
                     batch.push_back(queue_.front());
                     queue_.pop_front();
@@ -101,6 +114,7 @@ public:
 private:
     bert_ctx *ctx_;
     int n_threads_, max_batch_, wait_us_;
+    int clients_ = 0;
     std::mutex mu_;
     std::condition_variable cv_in_, cv_out_;
     std::deque<Request *> queue_;
@@ -123,6 +137,7 @@ void serve(int fd, bert_ctx *ctx, Batcher *b)
     const int32_t n_embd = bert_n_embd(ctx), n_max = bert_n_max_tokens(ctx);
     int one = 1;
     setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+    b->connected(+1);
     if (send_all(fd, &n_embd, sizeof(n_embd))) {
         std::vector<char> buf((size_t)1 << 15);      // server.cpp:27
         for (;;) {
@@ -137,6 +152,7 @@ void serve(int fd, bert_ctx *ctx, Batcher *b)
             if (!send_all(fd, r.emb.data(), r.emb.size() * sizeof(float))) break;
         }
     }
+    b->connected(-1);
     close(fd);
 }
 
