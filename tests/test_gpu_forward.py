@@ -203,6 +203,20 @@ def test_survey_config(tmp_path, cfg):
     c = cosines(full[check], ref)
     print(cfg, "min cos vs oracle", c.min())
     assert np.all(c >= 1 - COS_TOL), c
+    if arch == "bge-large-en-v1.5":
+        # the library's in-process split (bert_abi.cpp run_forward) at C4 dims: two
+        # replicas (BERT_DEVICES=0,0, own streams and workspaces) give the bits of one
+        os.environ["BERT_DEVICES"] = "0,0"
+        try:
+            m2 = bertpy.BertModel(path)
+            assert m2.lib.bertx_num_devices(m2.ctx) == 2
+            two = m2.forward_batch(ids)
+            split = [p[1] for p in m2.device_last_call()]
+            del m2
+        finally:
+            os.environ["BERT_DEVICES"] = "0"
+        assert split == [16, 16], split
+        assert np.array_equal(two, full)
 
 
 def _hip():
