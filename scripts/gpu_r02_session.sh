@@ -7,7 +7,7 @@ TAG=${TAG:-r02e}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp PARITY_LOG=$OUT/parity.jsonl
-STEPS=${STEPS:-"test bench tok server inproc pmc"}
+STEPS=${STEPS:-"test bench prof tok server inproc pmc"}
 has() { [[ " $STEPS " == *" $1 "* ]]; }
 step() { local lim=$1; shift; timeout -k 10 $lim "$@"; }
 if has test; then
@@ -15,6 +15,9 @@ if has test; then
   tail -2 $OUT/gputest.log
 fi
 if has bench; then step 400 python bench.py > $OUT/bench.log 2>&1 || { tail -20 $OUT/bench.log; exit 1; }; fi
+if has prof; then
+  ( cd /tmp && step 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --steps 10 > $GRAFT_REPO_ROOT/$OUT/prof.log 2>&1 ) || { tail -20 $OUT/prof.log; exit 1; }
+fi
 if has inproc; then
   BERT_DEVICES=0,0 step 600 python -u bench.py --inproc --gpus 2 --steps 5 --warmup 1 > $OUT/inproc.log 2>&1 || { tail -20 $OUT/inproc.log; exit 1; }
   BERT_DEVICES=0 step 600 python -u bench.py --inproc --gpus 1 --steps 5 --warmup 1 >> $OUT/inproc.log 2>&1 || { tail -20 $OUT/inproc.log; exit 1; }
