@@ -184,7 +184,9 @@ def probes(lib, bertpy, torch, a, dev, stream, q4_path):
                        "dominant_kernel": name, "avg_launch_us": round(avg_s * 1e6, 2),
                        "achieved_tflops": round(ach, 1), "peak_tflops": MFMA_F16_PEAK_TFLOPS,
                        "mfma_frac": round(ach / MFMA_F16_PEAK_TFLOPS, 4),
-                       "step_tflops": round(32 * flop_per_sentence(hp, 128) * steps / el / 1e12, 1)}
+                       "step_tflops": round(32 * flop_per_sentence(hp, 128) * steps / el / 1e12, 1),
+                       "kernel_avg_us": {s["name"]: round(s["ms"] * 1e3 / s["launches"], 2)
+                                         for s in st if s["launches"]}}
     del f
     # bandwidth probe: bge-base q4_0, one sentence of 32 tokens
     hp = bertpy.ARCHS["bge-base-en-v1.5"]
@@ -204,7 +206,9 @@ def probes(lib, bertpy, torch, a, dev, stream, q4_path):
                        "latency_us": round(lat * 1e6, 1), "algorithmic_bytes": int(by),
                        "achieved_gbps": round(by / lat / 1e9, 1), "peak_gbps": HBM_PEAK_GBPS,
                        "hbm_frac": round(by / lat / 1e9 / HBM_PEAK_GBPS, 4),
-                       "kernels_per_forward": launches, "sum_kernel_us": round(kern_s * 1e6, 1)}
+                       "kernels_per_forward": launches, "sum_kernel_us": round(kern_s * 1e6, 1),
+                       "kernel_avg_us": {s["name"]: round(s["ms"] * 1e3 / s["launches"], 2)
+                                         for s in st if s["launches"]}}
     pmc = os.path.join(ROOT, "profiles", "r02_probe_q4_0_b1_pmc.json")
     if os.path.exists(pmc):
         try:

@@ -125,7 +125,8 @@ class BertModel:
             sentences = [sentences]
         n = len(sentences)
         embeddings = np.zeros((n, self.n_embd), dtype=np.float32)
-        ptrs = (c_f32p * n)(*[e.ctypes.data_as(c_f32p) for e in embeddings])
+        ptrs = (embeddings.ctypes.data + embeddings.strides[0] * np.arange(n, dtype=np.uintp)).astype(np.uintp)
+        ptrs = ptrs.ctypes.data_as(ctypes.POINTER(c_f32p))
         texts = (ctypes.c_char_p * n)()
         for j, s in enumerate(sentences):
             texts[j] = s.encode("utf-8") if isinstance(s, str) else s
@@ -147,13 +148,21 @@ class BertModel:
 
     def forward_batch(self, ids_list, fake=False, fill=0.0):
         n = len(ids_list)
-        arrs = [np.ascontiguousarray(np.asarray(x, np.int32)) for x in ids_list]
-        lens = np.asarray([len(x) for x in arrs], np.int32)
+        lens = np.fromiter((len(x) for x in ids_list), np.int32, n)
+        flat = (np.concatenate(ids_list) if n else np.zeros(0)).astype(np.int32, copy=False)
+        flat = np.ascontiguousarray(flat)
         out = np.full((n, self.n_embd), fill, np.float32)
-        tp = (c_i32p * n)(*[_as_i32p(a) for a in arrs])
-        op = (c_f32p * n)(*[o.ctypes.data_as(c_f32p) for o in out])
+        # the int32_t* / float* arrays as address vectors into one id buffer and the
+        # output rows (a ctypes pointer object per row costs ~6 us: 0.4 ms for a
+        # 64-sentence batch, 5% of the forward)
+        offs = np.zeros(n, np.uintp)
+        if n > 1:
+            np.cumsum(lens[:-1], out=offs[1:])
+        tp = (flat.ctypes.data + 4 * offs).astype(np.uintp)
+        op = (out.ctypes.data + out.strides[0] * np.arange(n, dtype=np.uintp)).astype(np.uintp)
         fn = self.lib.bert_forward_fake_batch if fake else self.lib.bert_forward_batch
-        fn(self.ctx, self.N_THREADS, n, tp, _as_i32p(lens), op)
+        fn(self.ctx, self.N_THREADS, n, tp.ctypes.data_as(ctypes.POINTER(c_i32p)), _as_i32p(lens),
+           op.ctypes.data_as(ctypes.POINTER(c_f32p)))
         return out
 
     def forward(self, ids):
