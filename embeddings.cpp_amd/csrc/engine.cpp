@@ -550,22 +550,11 @@ int Device::launch_all(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, in
     const int G = d / 32;
 
     const double att_flop = att_flop_;   // sum over sentences of 4 d len^2 (QK^T and PV), set by the caller
-    // the projections that read the stream combine its statistics from the last
-    // residual GEMM's partials in their prologue and store them to st_ (the next
-    // residual GEMM's res_stats); layer 0's come from the embedding kernel
-    auto in_fold = [&](const float *c1, bool from_part) {
-        LnFold f;
-        f.c1 = c1;
-        if (from_part) {
-            f.in_part = part_; f.in_groups = G; f.in_part_stride = (int32_t)rows_; f.st_out = st_;
-        } else {
-            f.in_stats = st_;
-        }
-        return f;
-    };
     for (int l = 0; l < hp_.n_layer; ++l) {
         const DevLayer &L = layers_[(size_t)l];
-        LnFold in = in_fold(L.c1_qkv, l > 0);
+        LnFold in;
+        in.in_stats = st_;
+        in.c1 = L.c1_qkv;
         begin(K_GEMM_QKV, s, ev);
         launch_gemm(L.qkv, z_, M, L.c2_qkv, EPI_BIAS_F16, nullptr, qkv_, s, in);
         end(K_GEMM_QKV, s, ev, 2.0 * t * 3.0 * d * d);
@@ -585,9 +574,12 @@ int Device::launch_all(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, in
         end(K_GEMM_O, s, ev, 2.0 * t * d * d);
         chk("gemm_o", l, z_, (size_t)T * d, 1);
 
+        begin(K_LN_STATS, s, ev);
+        launch_ln_stats(part_, G, (int32_t)rows_, M, d, st_, s);
+        end(K_LN_STATS, s, ev, (double)M * (G + 1) * 8.0);
         gz = L.ln1_w; bz = L.ln1_b;
 
-        in = in_fold(L.c1_up, true);
+        in.c1 = L.c1_up;
         begin(K_GEMM_FFN_UP, s, ev);
         launch_gemm(L.up, z_, M, L.c2_up, EPI_BIAS_GELU_F16, nullptr, ffn_, s, in);
         end(K_GEMM_FFN_UP, s, ev, 2.0 * t * d * f);
@@ -601,12 +593,11 @@ int Device::launch_all(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, in
         end(K_GEMM_FFN_DOWN, s, ev, 2.0 * t * d * f);
         chk("gemm_down", l, z_, (size_t)T * d, 1);
 
+        begin(K_LN_STATS, s, ev);
+        launch_ln_stats(part_, G, (int32_t)rows_, M, d, st_, s);
+        end(K_LN_STATS, s, ev, (double)M * (G + 1) * 8.0);
         gz = L.ln2_w; bz = L.ln2_b;
     }
-    // the last stream's statistics for the pool
-    begin(K_LN_STATS, s, ev);
-    launch_ln_stats(part_, G, (int32_t)rows_, M, d, st_, s);
-    end(K_LN_STATS, s, ev, (double)M * (G + 1) * 8.0);
     begin(K_POOL_L2, s, ev);
     launch_pool_l2(z_, st_, gz, bz, d_cu, n_seqs, max_len, d, pool_part_, d_out, s);
     end(K_POOL_L2, s, ev, t * d * 2.0 + t * 8.0 + (double)n_seqs * d * 4.0);
@@ -709,20 +700,18 @@ extern "C" int32_t bertx_test_gemm(int32_t fmt, int32_t N, int32_t K, const void
                                    int32_t M, const uint16_t *x, int32_t epi, const void *res, void *out,
                                    int32_t cfg)
 {
-    return bertx_test_gemm_ln(fmt, N, K, w_rows, bias, M, x, nullptr, nullptr, nullptr, nullptr, epi,
-                              (const uint16_t *)res, nullptr, nullptr, nullptr, nullptr, (uint16_t *)out, nullptr, cfg);
+    return bertx_test_gemm_ln(fmt, N, K, w_rows, bias, M, x, nullptr, nullptr, nullptr, epi, (const uint16_t *)res,
+                              nullptr, nullptr, nullptr, nullptr, (uint16_t *)out, nullptr, cfg);
 }
 
 extern "C" int32_t bertx_test_gemm_ln(int32_t fmt, int32_t N, int32_t K, const void *w_rows, const float *bias,
-                                      int32_t M, const uint16_t *x, const float *in_stats, const float *in_part,
-                                      const float *in_g, const float *in_b, int32_t epi, const uint16_t *res,
-                                      const float *res_stats, const float *res_g, const float *res_b,
-                                      const float *g_next, uint16_t *out, float *st_out, int32_t cfg)
+                                      int32_t M, const uint16_t *x, const float *in_stats, const float *in_g,
+                                      const float *in_b, int32_t epi, const uint16_t *res, const float *res_stats,
+                                      const float *res_g, const float *res_b, const float *g_next, uint16_t *out,
+                                      float *st_out, int32_t cfg)
 {
     using namespace emb;
     if (!fmt_valid(fmt) || K % 64 || N % 32 || M <= 0 || epi < 0 || epi > 2 || hip_device_count() == 0) return -1;
-    if (in_stats && in_part) return -1;
-    if (in_part) in_stats = in_part;   // validated as the input-fold case below
     if ((in_stats && (!in_g || !in_b || epi == EPI_BIAS_RES)) || (epi == EPI_BIAS_RES && !res) ||
         (res_stats && (!res_g || !res_b)) || (g_next && epi != EPI_BIAS_RES))
         return -1;
@@ -740,18 +729,7 @@ extern "C" int32_t bertx_test_gemm_ln(int32_t fmt, int32_t N, int32_t K, const v
         const HostTensor hb = vec_tensor(bias, N), hg = vec_tensor(in_g, K), hbt = vec_tensor(in_b, K);
         Piece c1, c2;
         fold_ln({&t}, {&hb}, hg, hbt, c1, c2, fmt == FMT_F32);
-        if (in_part != nullptr) {
-            // the partials [K/32][M] float pairs, restrided to the padded rows
-            std::vector<float> pp((size_t)(K / 32) * Mp * 2, 0.f);
-            for (int gi = 0; gi < K / 32; ++gi)
-                std::memcpy(pp.data() + (size_t)gi * Mp * 2, in_part + (size_t)gi * M * 2, (size_t)M * 8);
-            ln.in_part = (const float2 *)B.up(pp.data(), pp.size() * 4, 0);
-            ln.in_groups = K / 32;
-            ln.in_part_stride = Mp;
-            ln.st_out = (float2 *)B.up(nullptr, 0, (size_t)Mp * 8);
-        } else {
-            ln.in_stats = (const float2 *)B.up(in_stats, (size_t)M * 8, (size_t)Mp * 8);
-        }
+        ln.in_stats = (const float2 *)B.up(in_stats, (size_t)M * 8, (size_t)Mp * 8);
         ln.c1 = (const float *)B.up(c1.bytes.data(), c1.bytes.size(), 0);
         dbias = (const float *)B.up(c2.bytes.data(), c2.bytes.size(), 0);
     }
@@ -784,7 +762,6 @@ extern "C" int32_t bertx_test_gemm_ln(int32_t fmt, int32_t N, int32_t K, const v
     HIP_RC(hipDeviceSynchronize());
     HIP_RC(hipMemcpy(out, dout, (size_t)M * N * 2, hipMemcpyDeviceToHost));
     if (dst && st_out) HIP_RC(hipMemcpy(st_out, dst, (size_t)M * 8, hipMemcpyDeviceToHost));
-    if (ln.st_out && st_out) HIP_RC(hipMemcpy(st_out, ln.st_out, (size_t)M * 8, hipMemcpyDeviceToHost));
     return 0;
 }
 
@@ -838,13 +815,7 @@ extern "C" int32_t bertx_bench_gemm(int32_t fmt, int32_t N, int32_t K, int32_t M
         ln.part = (float2 *)B.up(nullptr, 0, (size_t)Mp * (N / 32) * 8);
         ln.part_stride = Mp;
     } else {
-        // production: statistics combined in the prologue from K/32 group partials
-        std::vector<float> pp((size_t)(K / 32) * Mp * 2);
-        for (size_t i = 0; i < pp.size(); i += 2) { pp[i] = (rnd() - 0.5f) * 4.0f; pp[i + 1] = 30.0f + rnd(); }
-        ln.in_part = (const float2 *)B.up(pp.data(), pp.size() * 4, 0);
-        ln.in_groups = K / 32;
-        ln.in_part_stride = Mp;
-        ln.st_out = (float2 *)B.up(nullptr, 0, (size_t)Mp * 8);
+        ln.in_stats = (const float2 *)B.up(hs.data(), hs.size() * 4, 0);
         ln.c1 = (const float *)B.up(hg.data(), (size_t)N * 4, 0);
     }
     if (B.bad) return -1;

@@ -95,7 +95,7 @@ __device__ __forceinline__ void zmma_items(const R &cur, uint32_t b0, uint32_t b
 // The tile body: workgroup b of a grid of nTiles tiles (nN column tiles),
 // staging X in `smem` (NS * BM * 128 B of LDS).
 template <int FMT, int EPI, bool LNF, int NW, int BM, int NS>
-__device__ __forceinline__ void gemmz_body(char *__restrict__ smem, float2 *__restrict__ stl, const int b, DevWeight W,
+__device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b, DevWeight W,
                                            const h16 *__restrict__ X, const float *__restrict__ bias,
                                            const void *__restrict__ res, void *__restrict__ out, int nN, int nTiles,
                                            const LnFold &ln)
@@ -154,27 +154,6 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, float2 *__re
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[a][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    // input side of the LN fold: the statistics of the tile's BM input rows, one row
-    // per thread, into LDS (stl) for the epilogue -- given (in_stats), or combined
-    // here from the residual GEMM's 32-feature partials (in_part; the statistics
-    // kernel's arithmetic), those loads issued ahead of the first K-steps' loads so
-    // the two latencies overlap; the column-0 tiles also store them (st_out)
-    constexpr bool INF = EPI != EPI_BIAS_RES && LNF;
-    constexpr int MAXG = 32;                    // d <= 1024
-    float2 pp[MAXG];
-    const bool strow = INF && tid < BM;
-    if constexpr (INF) {
-        if (strow) {
-            if (ln.in_part) {
-#pragma unroll
-                for (int gi = 0; gi < MAXG; ++gi)
-                    if (gi < ln.in_groups) pp[gi] = ln.in_part[(size_t)gi * ln.in_part_stride + m0 + tid];
-            } else {
-                pp[0] = ln.in_stats[m0 + tid];
-            }
-        }
-    }
-
     ZRegs<FMT> w0, w1, w2;
     const int k1 = min(1, KS - 1);
     wload(w0, 0);
@@ -195,29 +174,6 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, float2 *__re
         asm volatile("" ::: "memory");
         issue_x(min(2, KS - 1), 2);
         wait_vmcnt<P + XG>();
-    }
-    if constexpr (INF) {
-        if (strow) {
-            float2 v = pp[0];
-            if (ln.in_part) {
-                const int G = ln.in_groups;
-                float sm = 0.f;
-#pragma unroll
-                for (int gi = 0; gi < MAXG; ++gi)
-                    if (gi < G) sm += pp[gi].x;
-                const float dd = (float)(32 * G), mean = sm / dd;
-                float m2 = 0.f;
-#pragma unroll
-                for (int gi = 0; gi < MAXG; ++gi)
-                    if (gi < G) {
-                        const float dm = pp[gi].x - 32.0f * mean;
-                        m2 += pp[gi].y + dm * dm * (1.0f / 32.0f);
-                    }
-                v = float2{mean, 1.0f / sqrtf(m2 / dd + 1e-5f)};
-                if (ln.st_out && n0 == 0) ln.st_out[m0 + tid] = v;
-            }
-            stl[tid] = v;
-        }
     }
     lds_barrier();
 
@@ -308,8 +264,7 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, float2 *__re
 #pragma unroll
         for (int jp = 0; jp < JC / 2; ++jp) {
             const int tok = m0 + 16 * (jc + 2 * jp + (g & 1)) + fr;
-            if constexpr (INF) sts[jp] = stl[tok - m0];
-            else if constexpr (use_st) sts[jp] = stp[tok];
+            if constexpr (use_st) sts[jp] = stp[tok];
             else sts[jp] = float2{0.f, 1.f};
             if constexpr (RES) {
 #pragma unroll
@@ -400,8 +355,7 @@ __global__ __launch_bounds__(64 * NW, 2) void gemmz_kernel(DevWeight W, const h1
                                                                int nN, int nTiles, LnFold ln)
 {
     __shared__ __attribute__((aligned(16))) char smem[NS * BM * ZK * 2];
-    __shared__ float2 stl[BM];
-    gemmz_body<FMT, EPI, LNF, NW, BM, NS>(smem, stl, blockIdx.x, W, X, bias, res, out, nN, nTiles, ln);
+    gemmz_body<FMT, EPI, LNF, NW, BM, NS>(smem, blockIdx.x, W, X, bias, res, out, nN, nTiles, ln);
 }
 
 template <int FMT, int NW, int BM, int NS>
@@ -465,11 +419,8 @@ int launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *b
     // LN + next gamma + partials
     const bool res_ln = ln.res_stats && ln.res_g && ln.res_b && ln.g_next && ln.part;
     if (epi == EPI_BIAS_RES && !res_ln && (ln.res_stats || ln.g_next)) return -1;
-    const bool in_ln = ln.in_stats || ln.in_part;
-    if (epi != EPI_BIAS_RES && in_ln && (!ln.c1 || (ln.in_part && (ln.in_groups < 1 || ln.in_groups > 32 ||
-                                                                  32 * ln.in_groups != W.K - (W.kx ? W.kx : 0)))))
-        return -1;
-    const bool lnf = epi == EPI_BIAS_RES ? res_ln : in_ln;
+    if (epi != EPI_BIAS_RES && ln.in_stats && !ln.c1) return -1;
+    const bool lnf = epi == EPI_BIAS_RES ? res_ln : ln.in_stats != nullptr;
     const int cfg = g_gemm_cfg;
     switch (W.fmt) {
     case FMT_Q4_0: launch_fmt<FMT_Q4_0>(W, x, M, bias, epi, res, out, s, ln, lnf, cfg); break;

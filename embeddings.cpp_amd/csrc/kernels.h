@@ -29,9 +29,8 @@
 //   * the mean pool: the same expression per token.
 // The statistics of a new stream y' come from the residual GEMM that produces
 // it: each wave's 32 features of a row give (sum, squared deviations from their
-// own mean) in its epilogue, and the next projection's prologue combines them
-// per row (Chan et al.; ln_stats does the same for the pool at the end).  No
-// kernel reads y' to normalise it.
+// own mean) in its epilogue, and ln_stats combines them per row (Chan et al.).
+// No kernel reads y' to normalise it.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -73,13 +72,6 @@ struct LnFold {
     // + bias[n], where the caller passes c2 as `bias`.  Null: plain acc + bias.
     const float2 *in_stats = nullptr;
     const float *c1 = nullptr;
-    // ... or the statistics combined in the GEMM's prologue from the 32-feature
-    // group partials a residual GEMM wrote (in_part[g * in_part_stride + row],
-    // g < in_groups = K / 32), and stored to st_out by the column-0 tiles (the next
-    // residual GEMM's res_stats) -- no separate statistics launch.
-    const float2 *in_part = nullptr;
-    int32_t in_groups = 0, in_part_stride = 0;
-    float2 *st_out = nullptr;
     // Residual side (EPI_BIAS_RES): `res` holds z of the previous LN (res_stats,
     // gamma res_g, beta res_b), the residual being LN(y) = r z - r mean gamma +
     // beta; res_stats null: the residual as stored.  With g_next the new stream

@@ -96,10 +96,6 @@ BERT_API int32_t bertx_test_gemm(int32_t fmt, int32_t N, int32_t K, const void *
  *  - in_stats (epi 0/1): x holds z = y * in_g of rows y with in_stats[M] =
  *    (mean, 1/sigma) float pairs; the result is LN(y) W^T + bias with LN's gamma
  *    in_g, beta in_b [K] (else NULL: plain x W^T + bias);
- *  - in_part instead of in_stats: y's statistics as the forward hands them over,
- *    [K/32][M] float pairs (sum, squared deviations from the group mean) of each
- *    32-feature group, combined in the GEMM's prologue; st_out [M] receives the
- *    combined (mean, 1/sigma);
  *  - epi 2: res holds z = y * res_g with res_stats [M] (the residual is LN(y) with
  *    gamma res_g, beta res_b [N]), or the plain residual when res_stats is NULL;
  *    with g_next [N] the output is f16(y' * g_next) of the new stream y' =
@@ -107,10 +103,10 @@ BERT_API int32_t bertx_test_gemm(int32_t fmt, int32_t N, int32_t K, const void *
  *    forward computes them (epilogue partials + the statistics kernel).
  */
 BERT_API int32_t bertx_test_gemm_ln(int32_t fmt, int32_t N, int32_t K, const void *w_rows, const float *bias,
-                                    int32_t M, const uint16_t *x, const float *in_stats, const float *in_part,
-                                    const float *in_g, const float *in_b, int32_t epi, const uint16_t *res,
-                                    const float *res_stats, const float *res_g, const float *res_b,
-                                    const float *g_next, uint16_t *out, float *st_out, int32_t cfg);
+                                    int32_t M, const uint16_t *x, const float *in_stats, const float *in_g,
+                                    const float *in_b, int32_t epi, const uint16_t *res, const float *res_stats,
+                                    const float *res_g, const float *res_b, const float *g_next, uint16_t *out,
+                                    float *st_out, int32_t cfg);
 
 /*
  * GEMM micro-benchmark on random operands (device 0): average device time of
