@@ -82,6 +82,50 @@ __device__ __forceinline__ uint32_t gelu2_era(float a, float b)
     return __builtin_bit_cast(uint32_t, x * r);
 }
 
+// Eight GELUs (four f16 pairs, the epilogue form): the arithmetic of gelu2_era
+// in one asm block, the four pairs interleaved so that no dependent
+// instruction follows its producer directly (no hazard wait states), and the
+// high halves of exp / rcp written in place by SDWA (no repacking).  o[i] =
+// the f16 pair gelu(v[2i]), gelu(v[2i+1]).
+__device__ __forceinline__ void gelu8_era(const float (&v)[8], uint32_t (&o)[4])
+{
+    const h16 c0 = (h16)(-2.0f * 1.4426950408889634f * 0.7978845608028654f);
+    const h16 c1 = (h16)(-2.0f * 1.4426950408889634f * 0.7978845608028654f * 0.044715f);
+    const uint32_t C1 = __builtin_bit_cast(uint32_t, h16x2{c1, c1});
+    const uint32_t C0 = __builtin_bit_cast(uint32_t, h16x2{c0, c0});
+    const uint32_t ONE = 0x3C003C00u;
+    uint32_t x0, x1, x2, x3, t0, t1, t2, t3;
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_cvt_pk_f16_f32 %4, %12, %13\n\tv_cvt_pk_f16_f32 %5, %14, %15\n\t"
+        "v_cvt_pk_f16_f32 %6, %16, %17\n\tv_cvt_pk_f16_f32 %7, %18, %19\n\t"
+        "v_pk_mul_f16 %8, %4, %4\n\tv_pk_mul_f16 %9, %5, %5\n\t"
+        "v_pk_mul_f16 %10, %6, %6\n\tv_pk_mul_f16 %11, %7, %7\n\t"
+        "v_pk_fma_f16 %8, %8, %20, %21\n\tv_pk_fma_f16 %9, %9, %20, %21\n\t"
+        "v_pk_fma_f16 %10, %10, %20, %21\n\tv_pk_fma_f16 %11, %11, %20, %21\n\t"
+        "v_pk_mul_f16 %8, %8, %4\n\tv_pk_mul_f16 %9, %9, %5\n\t"
+        "v_pk_mul_f16 %10, %10, %6\n\tv_pk_mul_f16 %11, %11, %7\n\t"
+        "v_exp_f16_e32 %0, %8\n\tv_exp_f16_e32 %1, %9\n\tv_exp_f16_e32 %2, %10\n\tv_exp_f16_e32 %3, %11\n\t"
+        "v_exp_f16_sdwa %0, %8 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1\n\t"
+        "v_exp_f16_sdwa %1, %9 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1\n\t"
+        "v_exp_f16_sdwa %2, %10 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1\n\t"
+        "v_exp_f16_sdwa %3, %11 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1\n\t"
+        "v_pk_add_f16 %8, %0, %22\n\tv_pk_add_f16 %9, %1, %22\n\t"
+        "v_pk_add_f16 %10, %2, %22\n\tv_pk_add_f16 %11, %3, %22\n\t"
+        "v_rcp_f16_e32 %0, %8\n\tv_rcp_f16_e32 %1, %9\n\tv_rcp_f16_e32 %2, %10\n\tv_rcp_f16_e32 %3, %11\n\t"
+        "v_rcp_f16_sdwa %0, %8 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1\n\t"
+        "v_rcp_f16_sdwa %1, %9 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1\n\t"
+        "v_rcp_f16_sdwa %2, %10 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1\n\t"
+        "v_rcp_f16_sdwa %3, %11 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1\n\t"
+        "v_pk_mul_f16 %0, %4, %0\n\tv_pk_mul_f16 %1, %5, %1\n\t"
+        "v_pk_mul_f16 %2, %6, %2\n\tv_pk_mul_f16 %3, %7, %3\n\t"
+        "s_nop 1"
+        : "=&v"(o[0]), "=&v"(o[1]), "=&v"(o[2]), "=&v"(o[3]), "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3),
+          "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3)
+        : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]), "s"(C1), "v"(C0),
+          "v"(ONE));
+}
+
 // LDS-DMA: `size` bytes per lane from the per-lane global address `g` into
 // LDS at (wave-uniform) `lds_base` + lane * size.
 template <int SIZE>

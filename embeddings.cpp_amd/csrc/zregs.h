@@ -135,5 +135,14 @@ __device__ __forceinline__ void zswap(float &x, float &y)
     asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
 }
 
+// The four exchanges (v[e], v[4 + e]) of one epilogue row pair behind a single
+// hazard pad (their operands are accumulators the K loop wrote long before).
+__device__ __forceinline__ void zswap4(float (&v)[8])
+{
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %4\n\tv_permlane16_swap_b32 %1, %5\n\t"
+                 "v_permlane16_swap_b32 %2, %6\n\tv_permlane16_swap_b32 %3, %7"
+                 : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]));
+}
+
 }  // namespace
 }  // namespace emb

@@ -64,7 +64,9 @@ def gelu_ref(acc):
                                    # 4 (2 waves 64x64)
                                    (768, 768, 512, 2), (2304, 768, 768, 2), (448, 192, 700, 3),
                                    (256, 3072, 256, 2), (2304, 192, 256, 2), (384, 1536, 200, 4),
-                                   (96, 768, 32, 4), (1152, 384, 64, 0)])
+                                   (96, 768, 32, 4), (1152, 384, 64, 0),
+                                   # 5: 4 waves 128 x 256, 64 features per wave (N % 256 != 0 too)
+                                   (768, 768, 512, 5), (1152, 384, 256, 5), (2304, 768, 384, 5)])
 def test_gemm_matches_numpy(lib, fmt, epi, shape):
     N, K, M, cfg = shape
     rng = np.random.default_rng(fmt * 10 + epi)
@@ -109,7 +111,7 @@ def f32p(a):
 @pytest.mark.parametrize("fmt", [0, 1, 2, 3, 8])
 @pytest.mark.parametrize("epi", [0, 1])
 @pytest.mark.parametrize("N,K,M,cfg", [(2304, 768, 512, 0), (384, 1536, 300, 3), (1024, 1024, 768, 2),
-                                       (1536, 384, 96, 4)])
+                                       (1536, 384, 96, 4), (3072, 768, 256, 5)])
 def test_gemm_input_ln_fold(lib, fmt, epi, N, K, M, cfg):
     """Projection of a LayerNorm'd stream as the forward runs it (kernels.h LN fold):
     the GEMM reads z = f16(y * gamma) and the row statistics of y, and returns
@@ -147,7 +149,7 @@ def test_gemm_input_ln_fold(lib, fmt, epi, N, K, M, cfg):
 
 @pytest.mark.parametrize("fmt", [1, 2, 3, 8])
 @pytest.mark.parametrize("N,K,M,cfg", [(768, 768, 512, 0), (384, 1536, 256, 3), (1024, 1024, 384, 2),
-                                       (768, 3072, 256, 0), (384, 1536, 130, 4)])
+                                       (768, 3072, 256, 0), (384, 1536, 130, 4), (768, 3072, 384, 5)])
 def test_residual_gemm_ln_statistics(lib, fmt, N, K, M, cfg):
     """Residual projection as the forward runs it: res = f16(y * gamma) with y's
     statistics (the residual is LN(y)), y' = LN(y) + x W^T + b comes back as
