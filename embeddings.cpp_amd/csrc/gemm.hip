@@ -343,28 +343,33 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
         }
         if (nxt) col8(3, gn);
         constexpr bool use_st = LNF;
-        // every residual row chunk and LN statistic of up to 8 token pairs in flight
-        // before the first use (one latency, not one per pair)
-        constexpr int JC = NJ < 16 ? NJ : 8;        // token groups per prefetch chunk
+        // token pairs j = 2 jp, 2 jp + 1 (after the exchange each lane holds one
+        // token of the pair); the residual rows of PW pairs stay in flight ahead
+        // of their use (a sliding window: one load latency per tile, not per pair)
+        constexpr int NP = NJ / 2, PW = NP < 4 ? NP : 4;
+        uint4 rr[PW][2];
+        auto ldres = [&](int jp) {
+            const int tok = m0 + 16 * (2 * jp + (g & 1)) + fr;
 #pragma unroll
-        for (int jc = 0; jc < NJ; jc += JC) {
-            uint4 rr[JC / 2][2];
-            float2 sts[JC / 2];
+            for (int a = 0; a < 2; ++a)
+                rr[jp % PW][a] = *(const uint4 *)((const h16 *)res + (size_t)tok * N + cb + 16 * a);
+        };
+        if constexpr (RES) {
 #pragma unroll
-            for (int jp = 0; jp < JC / 2; ++jp) {
-                const int tok = m0 + 16 * (jc + 2 * jp + (g & 1)) + fr;
-                if constexpr (use_st) sts[jp] = estat[tok - m0];
-                else sts[jp] = float2{0.f, 1.f};
-                if constexpr (RES) {
+            for (int jp = 0; jp < PW; ++jp) ldres(jp);
+        }
 #pragma unroll
-                    for (int a = 0; a < 2; ++a)
-                        rr[jp][a] = *(const uint4 *)((const h16 *)res + (size_t)tok * N + cb + 16 * a);
-                }
-            }
-#pragma unroll
-            for (int j = jc; j < jc + JC; j += 2) {
+        for (int jp = 0; jp < NP; ++jp) {
+            {
+                const int j = 2 * jp;
                 const int tok = m0 + 16 * (j + (g & 1)) + fr;
-                const float2 stt = sts[(j - jc) >> 1];
+                const float2 stt = use_st ? estat[tok - m0] : float2{0.f, 1.f};
+                uint4 rcur[2] = {};
+                if constexpr (RES) {
+                    rcur[0] = rr[jp % PW][0];
+                    rcur[1] = rr[jp % PW][1];
+                    if (jp + PW < NP) ldres(jp + PW);
+                }
                 // (mean, 1/sigma) -> v = r x + t with t = -mean / sigma
                 const float sr = stt.y, st0 = -stt.x * stt.y;
                 float v[2][8];
@@ -389,7 +394,7 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
                 } else {
 #pragma unroll
                     for (int a = 0; a < 2; ++a) {
-                        const h16x8 rh = __builtin_bit_cast(h16x8, rr[(j - jc) >> 1][a]);
+                        const h16x8 rh = __builtin_bit_cast(h16x8, rcur[a]);
 #pragma unroll
                         for (int e = 0; e < 8; ++e) {
                             const float z = (float)rh[e], bv = bb[a][e >> 2][e & 3];
