@@ -122,6 +122,10 @@ private:
     void mark_done(hipStream_t s);          // records the completion event of a forward on s
     int launch_all(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, int max_len, int T, float *d_out,
                    hipStream_t s, bool check);
+    // One chain of the forward over sentences seq0 .. seq0 + n_seqs - 1, whose
+    // tokens are rows row0 .. row0 + T - 1 (d_cu / d_out already offset to seq0).
+    void launch_chain(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, int max_len, int T, int64_t row0,
+                      int64_t seq0, float *d_out, hipStream_t s, bool check, bool &bad, unsigned *cnt);
     void drop_graphs();
     void upload(const HostModel &m);
     void *arena_alloc(size_t bytes);
@@ -133,6 +137,9 @@ private:
     int ordinal_ = 0;
     HParams hp_;
     hipStream_t stream_ = nullptr;
+    static constexpr int kMaxChains = 4;
+    hipStream_t chain_s_[kMaxChains] = {};   // chains 1.. of a split forward (chain 0: the caller's stream)
+    hipEvent_t fork_ev_ = nullptr, join_ev_[kMaxChains] = {};
     std::mutex mu_;
 
     // weights
