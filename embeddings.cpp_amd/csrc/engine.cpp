@@ -219,17 +219,10 @@ Device::Device(int ordinal, const HostModel &m) : ordinal_(ordinal), hp_(m.hp)
 {
     DeviceGuard g(ordinal);
     if (!g.ok() || hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&fork_ev_, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&done_ev_, hipEventDisableTiming) != hipSuccess) {
         std::fprintf(stderr, "libbert: cannot initialise HIP device %d\n", ordinal);
         return;
     }
-    for (int c = 1; c < kMaxChains; ++c)
-        if (hipStreamCreateWithFlags(&chain_s_[c], hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&join_ev_[c], hipEventDisableTiming) != hipSuccess) {
-            std::fprintf(stderr, "libbert: cannot create the chain streams of HIP device %d\n", ordinal);
-            return;
-        }
     upload(m);
 }
 
@@ -246,14 +239,7 @@ Device::~Device()
     if (h_ids_) (void)hipHostFree(h_ids_);
     if (h_cu_) (void)hipHostFree(h_cu_);
     if (h_out_) (void)hipHostFree(h_out_);
-    for (auto cs : chain_s_)
-        if (cs) (void)hipStreamSynchronize(cs);
     if (done_ev_) (void)hipEventDestroy(done_ev_);
-    if (fork_ev_) (void)hipEventDestroy(fork_ev_);
-    for (auto e : join_ev_)
-        if (e) (void)hipEventDestroy(e);
-    for (auto cs : chain_s_)
-        if (cs) (void)hipStreamDestroy(cs);
     if (stream_) (void)hipStreamDestroy(stream_);
 }
 
@@ -531,76 +517,16 @@ int Device::forward_ordered(const int32_t *d_ids, const int32_t *d_cu, int n_seq
     return hipGraphLaunch(exec, s) == hipSuccess ? 0 : -1;
 }
 
-// Chains: a batch of equal-length sentences whose 1/n parts are whole GEMM
-// tiles runs as n independent forwards (consecutive sentence ranges) on the
-// caller's stream and chain_s_[1..n-1], forked and joined by events (captured
-// into the same graph).  Their kernels share no rows, so one chain's kernels fill
-// the CUs another's leave idle -- the last, partial round of tiles of a GEMM
-// (O-proj and FFN-down have 1.5 rounds at C3), the statistics launches and the
-// gaps between dependent launches.  BERT_CHAINS = n (default 2; 1 = off).
-static int chains_env()
-{
-    static const int n = [] {
-        const char *e = std::getenv("BERT_CHAINS");
-        const int v = e && *e ? std::atoi(e) : 2;
-        return v < 1 ? 1 : v;
-    }();
-    return n;
-}
-
 int Device::launch_all(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, int max_len, int T, float *d_out,
                        hipStream_t s, bool check)
-{
-    unsigned *cnt = nullptr;
-    bool bad = false;
-    if (check) (void)hipMalloc((void **)&cnt, sizeof(unsigned));
-    int nch = std::min(chains_env(), (int)kMaxChains);
-    const auto fits = [&](int n) {
-        const int part = T / n;
-        return n_seqs % n == 0 && (int64_t)n_seqs * max_len == T && part >= GEMM_PAD_BIG && gemm_rows(part) == part;
-    };
-    while (nch > 1 && !fits(nch)) --nch;
-    if (check || profiling_ || s == nullptr) nch = 1;
-    if (nch > 1) {
-        const int ns = n_seqs / nch, part = T / nch, d = hp_.n_embd;
-        (void)hipEventRecord(fork_ev_, s);
-        for (int c = 1; c < nch; ++c) (void)hipStreamWaitEvent(chain_s_[c], fork_ev_, 0);
-        // stage by stage (embeddings, 2 per layer, pool), free-running: making the
-        // chains wait for each other (every half-layer, or a bounded lag) measured
-        // 3-13 % slower -- each cross-stream wait stalls a queue
-        for (int stg = 0; stg < n_stages(); ++stg)
-            for (int c = 0; c < nch; ++c)
-                launch_chain(d_ids, d_cu + (size_t)c * ns, ns, max_len, part, (int64_t)c * part, (int64_t)c * ns,
-                             d_out + (size_t)c * ns * d, c ? chain_s_[c] : s, false, bad, cnt, stg);
-        for (int c = 1; c < nch; ++c) {
-            (void)hipEventRecord(join_ev_[c], chain_s_[c]);
-            (void)hipStreamWaitEvent(s, join_ev_[c], 0);
-        }
-    } else {
-        for (int stg = 0; stg < n_stages(); ++stg)
-            launch_chain(d_ids, d_cu, n_seqs, max_len, T, 0, 0, d_out, s, check, bad, cnt, stg);
-    }
-    if (cnt) (void)hipFree(cnt);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) {
-        std::fprintf(stderr, "libbert: kernel launch failed: %s\n", hipGetErrorString(e));
-        return -1;
-    }
-    return 0;
-}
-
-void Device::launch_chain(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, int max_len, int T, int64_t row0,
-                          int64_t seq0, float *d_out, hipStream_t s, bool check, bool &bad, unsigned *cnt, int stage)
 {
     const int d = hp_.n_embd, f = hp_.n_intermediate;
     const int M = gemm_rows(T);   // GEMM rows: T padded to whole tiles
     const double t = (double)T;
     hipEvent_t ev;
-    // this chain's rows (cu holds absolute rows: embed, attention and pool index
-    // the full buffers)
-    uint16_t *const z = z_ + row0 * d, *const qkv = qkv_ + row0 * 3 * d, *const att = att_ + row0 * d;
-    uint16_t *const ffn = ffn_ + row0 * f;
-    float2 *const st = st_ + row0, *const part = part_ + row0;
+    unsigned *cnt = nullptr;
+    bool bad = false;
+    if (check) (void)hipMalloc((void **)&cnt, sizeof(unsigned));
     auto chk = [&](const char *what, int layer, const void *p, size_t n, int f16) {
         if (!check || bad) return;
         (void)hipMemsetAsync(cnt, 0, sizeof(unsigned), s);
@@ -613,81 +539,76 @@ void Device::launch_chain(const int32_t *d_ids, const int32_t *d_cu, int n_seqs,
             std::fprintf(stderr, "libbert: BERT_CHECK_FINITE: %u non-finite values after %s (layer %d)\n", h, what, layer);
         }
     };
-    const int nl = hp_.n_layer, G = d / 32;
+
+    begin(K_EMBED_LN, s, ev);
+    launch_embed_ln(word_, type_, pos_, ln_e_w_, d_ids, d_cu, n_seqs, max_len, d, z_, st_, s);
+    end(K_EMBED_LN, s, ev, t * (4.0 + 3.0 * d * 2.0 + 2.0 * d + 8.0));
+    chk("embed_ln", -1, z_, (size_t)T * d, 1);
     // z_ holds the stream as z = y * gamma of the LN in front of the next
-    // projection, st_ its (mean, 1/sigma) (kernels.h LN fold); (gz, bz) is that
-    // LN: the embeddings' in front of layer 0, else the previous layer's second
-    const auto ln_in = [&](int l, const float *&gz, const float *&bz) {
-        gz = l == 0 ? ln_e_w_ : layers_[(size_t)l - 1].ln2_w;
-        bz = l == 0 ? ln_e_b_ : layers_[(size_t)l - 1].ln2_b;
-    };
-    if (stage == 0) {
-        begin(K_EMBED_LN, s, ev);
-        launch_embed_ln(word_, type_, pos_, ln_e_w_, d_ids, d_cu, n_seqs, max_len, d, z_, st_, s);
-        end(K_EMBED_LN, s, ev, t * (4.0 + 3.0 * d * 2.0 + 2.0 * d + 8.0));
-        chk("embed_ln", -1, z, (size_t)T * d, 1);
-        return;
-    }
-    if (stage == 2 * nl + 1) {
-        const float *gz, *bz;
-        ln_in(nl, gz, bz);
-        begin(K_POOL_L2, s, ev);
-        launch_pool_l2(z_, st_, gz, bz, d_cu, n_seqs, max_len, d, pool_part_ + seq0 * pool_chunks(max_len) * d, d_out,
-                       s);
-        end(K_POOL_L2, s, ev, t * d * 2.0 + t * 8.0 + (double)n_seqs * d * 4.0);
-        chk("pool_l2", -1, d_out, (size_t)n_seqs * d, 0);
-        return;
-    }
-    const int l = (stage - 1) / 2;
-    const DevLayer &L = layers_[(size_t)l];
-    const float *gz, *bz;
-    ln_in(l, gz, bz);
-    LnFold in;
-    in.in_stats = st;
-    if ((stage - 1) % 2 == 0) {   // first half-layer: QKV and attention
+    // projection, st_ its (mean, 1/sigma) (kernels.h LN fold); (gz, bz) is that LN
+    const float *gz = ln_e_w_, *bz = ln_e_b_;
+    const int G = d / 32;
+
+    const double att_flop = att_flop_;   // sum over sentences of 4 d len^2 (QK^T and PV), set by the caller
+    for (int l = 0; l < hp_.n_layer; ++l) {
+        const DevLayer &L = layers_[(size_t)l];
+        LnFold in;
+        in.in_stats = st_;
         in.c1 = L.c1_qkv;
         begin(K_GEMM_QKV, s, ev);
-        launch_gemm(L.qkv, z, M, L.c2_qkv, EPI_BIAS_F16, nullptr, qkv, s, in);
+        launch_gemm(L.qkv, z_, M, L.c2_qkv, EPI_BIAS_F16, nullptr, qkv_, s, in);
         end(K_GEMM_QKV, s, ev, 2.0 * t * 3.0 * d * d);
-        chk("gemm_qkv", l, qkv, (size_t)T * 3 * d, 1);
+        chk("gemm_qkv", l, qkv_, (size_t)T * 3 * d, 1);
 
         begin(K_ATTENTION, s, ev);
         launch_attention(qkv_, d_cu, n_seqs, max_len, hp_.n_head, d, att_, s);
-        end(K_ATTENTION, s, ev, att_flop_);   // sum over sentences of 4 d len^2, set by the caller
-        chk("attention", l, att, (size_t)T * d, 1);
-        return;
+        end(K_ATTENTION, s, ev, att_flop);
+        chk("attention", l, att_, (size_t)T * d, 1);
+
+        // y1 = LN(y) + ATT W_o^T + b_o, stored as z = y1 * gamma_1 with its partials
+        LnFold r1;
+        r1.res_stats = st_; r1.res_g = gz; r1.res_b = bz;
+        r1.g_next = L.ln1_w; r1.part = part_; r1.part_stride = (int32_t)rows_;
+        begin(K_GEMM_O, s, ev);
+        launch_gemm(L.o, att_, M, L.b_o, EPI_BIAS_RES, z_, z_, s, r1);
+        end(K_GEMM_O, s, ev, 2.0 * t * d * d);
+        chk("gemm_o", l, z_, (size_t)T * d, 1);
+
+        begin(K_LN_STATS, s, ev);
+        launch_ln_stats(part_, G, (int32_t)rows_, M, d, st_, s);
+        end(K_LN_STATS, s, ev, (double)M * (G + 1) * 8.0);
+        gz = L.ln1_w; bz = L.ln1_b;
+
+        in.c1 = L.c1_up;
+        begin(K_GEMM_FFN_UP, s, ev);
+        launch_gemm(L.up, z_, M, L.c2_up, EPI_BIAS_GELU_F16, nullptr, ffn_, s, in);
+        end(K_GEMM_FFN_UP, s, ev, 2.0 * t * d * f);
+        chk("gemm_up", l, ffn_, (size_t)T * f, 1);
+
+        LnFold r2;
+        r2.res_stats = st_; r2.res_g = gz; r2.res_b = bz;
+        r2.g_next = L.ln2_w; r2.part = part_; r2.part_stride = (int32_t)rows_;
+        begin(K_GEMM_FFN_DOWN, s, ev);
+        launch_gemm(L.down, ffn_, M, L.b_down, EPI_BIAS_RES, z_, z_, s, r2);
+        end(K_GEMM_FFN_DOWN, s, ev, 2.0 * t * d * f);
+        chk("gemm_down", l, z_, (size_t)T * d, 1);
+
+        begin(K_LN_STATS, s, ev);
+        launch_ln_stats(part_, G, (int32_t)rows_, M, d, st_, s);
+        end(K_LN_STATS, s, ev, (double)M * (G + 1) * 8.0);
+        gz = L.ln2_w; bz = L.ln2_b;
     }
-    // second half-layer: y1 = LN(y) + ATT W_o^T + b_o, stored as z = y1 * gamma_1
-    // with its partials; the FFN on LN_1(y1), y2 = LN_1(y1) + FFN, z = y2 * gamma_2
-    LnFold r1;
-    r1.res_stats = st; r1.res_g = gz; r1.res_b = bz;
-    r1.g_next = L.ln1_w; r1.part = part; r1.part_stride = (int32_t)rows_;
-    begin(K_GEMM_O, s, ev);
-    launch_gemm(L.o, att, M, L.b_o, EPI_BIAS_RES, z, z, s, r1);
-    end(K_GEMM_O, s, ev, 2.0 * t * d * d);
-    chk("gemm_o", l, z, (size_t)T * d, 1);
-
-    begin(K_LN_STATS, s, ev);
-    launch_ln_stats(part, G, (int32_t)rows_, M, d, st, s);
-    end(K_LN_STATS, s, ev, (double)M * (G + 1) * 8.0);
-
-    in.c1 = L.c1_up;
-    begin(K_GEMM_FFN_UP, s, ev);
-    launch_gemm(L.up, z, M, L.c2_up, EPI_BIAS_GELU_F16, nullptr, ffn, s, in);
-    end(K_GEMM_FFN_UP, s, ev, 2.0 * t * d * f);
-    chk("gemm_up", l, ffn, (size_t)T * f, 1);
-
-    LnFold r2;
-    r2.res_stats = st; r2.res_g = L.ln1_w; r2.res_b = L.ln1_b;
-    r2.g_next = L.ln2_w; r2.part = part; r2.part_stride = (int32_t)rows_;
-    begin(K_GEMM_FFN_DOWN, s, ev);
-    launch_gemm(L.down, ffn, M, L.b_down, EPI_BIAS_RES, z, z, s, r2);
-    end(K_GEMM_FFN_DOWN, s, ev, 2.0 * t * d * f);
-    chk("gemm_down", l, z, (size_t)T * d, 1);
-
-    begin(K_LN_STATS, s, ev);
-    launch_ln_stats(part, G, (int32_t)rows_, M, d, st, s);
-    end(K_LN_STATS, s, ev, (double)M * (G + 1) * 8.0);
+    begin(K_POOL_L2, s, ev);
+    launch_pool_l2(z_, st_, gz, bz, d_cu, n_seqs, max_len, d, pool_part_, d_out, s);
+    end(K_POOL_L2, s, ev, t * d * 2.0 + t * 8.0 + (double)n_seqs * d * 4.0);
+    chk("pool_l2", -1, d_out, (size_t)n_seqs * d, 0);
+    if (cnt) (void)hipFree(cnt);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        std::fprintf(stderr, "libbert: kernel launch failed: %s\n", hipGetErrorString(e));
+        return -1;
+    }
+    return 0;
 }
 
 int Device::forward_host(const int32_t *const *tokens, const int32_t *lens, int n, float *const *out)

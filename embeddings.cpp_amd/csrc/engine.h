@@ -122,13 +122,6 @@ private:
     void mark_done(hipStream_t s);          // records the completion event of a forward on s
     int launch_all(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, int max_len, int T, float *d_out,
                    hipStream_t s, bool check);
-    // One chain of the forward over sentences seq0 .. seq0 + n_seqs - 1, whose
-    // tokens are rows row0 .. row0 + T - 1 (d_cu / d_out already offset to seq0).
-    // Stages: 0 embeddings, 2l + 1 QKV + attention of layer l, 2l + 2 the rest of
-    // layer l, 2 n_layer + 1 the pool.
-    void launch_chain(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, int max_len, int T, int64_t row0,
-                      int64_t seq0, float *d_out, hipStream_t s, bool check, bool &bad, unsigned *cnt, int stage);
-    int n_stages() const { return 2 * hp_.n_layer + 2; }
     void drop_graphs();
     void upload(const HostModel &m);
     void *arena_alloc(size_t bytes);
@@ -140,9 +133,6 @@ private:
     int ordinal_ = 0;
     HParams hp_;
     hipStream_t stream_ = nullptr;
-    static constexpr int kMaxChains = 4;
-    hipStream_t chain_s_[kMaxChains] = {};   // chains 1.. of a split forward (chain 0: the caller's stream)
-    hipEvent_t fork_ev_ = nullptr, join_ev_[kMaxChains] = {};
     std::mutex mu_;
 
     // weights

@@ -85,21 +85,6 @@ def test_batch_composition_invariance(quant_models):
     assert np.array_equal(rev[::-1], full)
 
 
-def test_two_chain_split_bitwise(quant_models):
-    """Equal-length batches whose halves are whole GEMM tiles run as two chains on two
-    streams (engine.cpp launch_all): every sentence, in either chain, is bitwise what
-    it is alone (no split), eagerly, captured and replayed."""
-    m = bertpy.BertModel(quant_models[("tiny64", "q4_0")])
-    ids = ragged_ids(690, [512] * 16, seed=9)
-    runs = [m.forward_batch(ids) for _ in range(3)]
-    for r in runs[1:]:
-        assert np.array_equal(r, runs[0])
-    for i in (0, 7, 8, 15):
-        assert np.array_equal(m.forward_batch([ids[i]])[0], runs[0][i])
-    o = oracle_lib.Oracle(quant_models[("tiny64", "q4_0")])
-    assert np.all(cosines(runs[0][[3, 12]], o.forward_batch([ids[3], ids[12]])) >= 1 - COS_TOL)
-
-
 def test_fake_batch_and_forward(quant_models):
     """bert_forward_fake_batch and bert_forward against the oracle's restatements
     (oracle_forward_fake_batch: bert.cpp:1151-1363; bert_forward = a batch of one,
@@ -151,7 +136,7 @@ def test_bge_base_q4_0_full_size(tmp_path):
     assert np.allclose(np.linalg.norm(full, axis=1), 1.0, atol=1e-5)
     two = m.forward_batch(ids[:2])
     assert np.array_equal(two, full[:2])
-    assert np.array_equal(m.forward_batch(ids[62:]), full[62:])    # the second chain's rows
+    assert np.array_equal(m.forward_batch(ids[62:]), full[62:])
     ref = oracle_lib.Oracle(path).forward_batch([ids[0], ids[1], ids[63]], n_threads=min(16, os.cpu_count() or 1))
     assert np.all(cosines(full[[0, 1, 63]], ref) >= 1 - COS_TOL)
 
