@@ -351,6 +351,22 @@ __device__ __forceinline__ int lane_id_opaque()
     return l;
 }
 
+#ifdef ATT_STAMPS
+// Diagnostic build only (make EXTRA=-DATT_STAMPS BUILD=...): per wave and item
+// (at most 4 items per workgroup) s_memtime at the item's start, after block 0,
+// at B1's arrival, after B1, at the block loop's end, after S, after the stores,
+// and the wave's HW_ID (scripts/att_stamps.py)
+__device__ unsigned long long g_att_stamps[1 << 17];
+#define ASTAMP(k, v) do { if (lane == 0 && nit < 4) g_att_stamps[(((size_t)blockIdx.x * 16 + w) * 4 + nit) * 8 + (k)] = (v); } while (0)
+extern "C" __attribute__((visibility("default"))) int bertx_att_stamps(unsigned long long *host, size_t n)
+{
+    if (n > (1u << 17)) n = 1u << 17;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_att_stamps), n * 8) == hipSuccess ? 0 : -1;
+}
+#else
+#define ASTAMP(k, v) do { } while (0)
+#endif
+
 __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restrict__ qkv,
                                                               const int32_t *__restrict__ cu, int d, int nh,
                                                               int n_items, float sl2, h16 *__restrict__ out)
@@ -544,7 +560,11 @@ __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restr
     issue(cur, 1);
     const h16 s16 = (h16)sl2;
     const h16x8 sc = {s16, s16, s16, s16, s16, s16, s16, s16};
+#ifdef ATT_STAMPS
+    int nit = 0;
+#endif
     for (;;) {
+        ASTAMP(0, __builtin_amdgcn_s_memtime());
         const int nx_i = cur_i + (int)gridDim.x;
         const bool more = nx_i < n_items;                 // workgroup-uniform
         Item nx = {0, 0, 0};
@@ -570,14 +590,17 @@ __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restr
             l = expsum();
             pv(0);
         }
+        ASTAMP(1, __builtin_amdgcn_s_memtime());
         bool qnext = false;
         // blocks 1-7 in one loop (one inlined copy of the block code), B1 at the
         // region boundary
 #pragma clang loop unroll(disable)
         for (int kb = 64; kb < LMAX; kb += 64) {
             if (kb == RH) {
+                ASTAMP(2, __builtin_amdgcn_s_memtime());
                 wait_vmcnt<0>();                          // this item's region-B pieces
                 __syncthreads();                          // B1: region A is free
+                ASTAMP(3, __builtin_amdgcn_s_memtime());
                 if (more) issue(nx, 0);
             }
             if (active && kb < nrows) {
@@ -589,25 +612,49 @@ __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restr
                 pv(kb);
             }
         }
+        ASTAMP(4, __builtin_amdgcn_s_memtime());
         if (more && !qnext) load_q(nx);
         wait_vmcnt<0>();                                  // the next item's region A and Q
         __syncthreads();                                  // S: region B is free
+        ASTAMP(5, __builtin_amdgcn_s_memtime());
         if (active) {
+            // lane (q, hi) holds dh 8m + 4 hi .. +3 of chunks m = 4t + g; one
+            // v_permlane32_swap per dword of the chunk pair (2p, 2p + 1) gives lane
+            // (q, 0) dh 16p .. 16p + 7 and lane (q, 1) dh 16p + 8 .. 16p + 15: four
+            // 16-B stores per lane instead of eight 8-B ones (the store tail is
+            // issue-bound; cdna_hip_programming.md T21).  Both lanes of a pair
+            // hold the same query, so the swaps run before the q < len test.
             const float inv = 1.0f / halves_sum(l);
             const int q = 32 * w + lq;
+            uint32_t pk[DH / 8][2];
+#pragma unroll
+            for (int m = 0; m < DH / 8; ++m)
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const int t = m >> 2, g = m & 3;
+                    const h16x2 v = {(h16)(o[t][4 * g + 2 * k] * inv), (h16)(o[t][4 * g + 2 * k + 1] * inv)};
+                    pk[m][k] = __builtin_bit_cast(uint32_t, v);
+                }
+#pragma unroll
+            for (int p = 0; p < DH / 16; ++p)
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const auto r = __builtin_amdgcn_permlane32_swap(pk[2 * p][k], pk[2 * p + 1][k], false, false);
+                    pk[2 * p][k] = r[0];
+                    pk[2 * p + 1][k] = r[1];
+                }
             if (q < len) {
-                h16 *orow = out + (size_t)(cur.start + q) * d + cur.h * DH;
+                h16 *orow = out + (size_t)(cur.start + q) * d + cur.h * DH + 8 * hi;
 #pragma unroll
-                for (int t = 0; t < DH / 32; ++t)
-#pragma unroll
-                    for (int g = 0; g < 4; ++g) {
-                        h16x4 v;
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) v[e] = (h16)(o[t][4 * g + e] * inv);
-                        *(h16x4 *)(orow + 32 * t + 8 * g + 4 * hi) = v;
-                    }
+                for (int p = 0; p < DH / 16; ++p)
+                    *(uint4 *)(orow + 16 * p) = uint4{pk[2 * p][0], pk[2 * p][1], pk[2 * p + 1][0], pk[2 * p + 1][1]};
             }
         }
+        ASTAMP(6, __builtin_amdgcn_s_memtime());
+#ifdef ATT_STAMPS
+        ASTAMP(7, (unsigned long long)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11)));
+        ++nit;
+#endif
         if (!more) break;
         issue(nx, 1);
         cur = nx;
