@@ -336,12 +336,12 @@ constexpr int ATT_SUMX = 12;   // a block whose half-row sum passes 2^ATT_SUMX m
 // image is two regions of 256 keys (A = key blocks 0-3, B = blocks 4-7):
 //   B1 (every wave past the item's region-A blocks): the next item's region-A
 //      K/V pieces are issued;
-//   S  (every wave past its region-B blocks): the item's rows are stored, then
-//      the next item's region-B pieces issued.
-// The vmcnt(0) in front of each barrier retires pieces issued half an item
-// earlier; only a workgroup's first item waits for its loads in the open.  The
-// next item's Q rows are read into the Q registers under the last block's P V
-// (its Q K^T, and any rescale, are done by then).
+//   S  (every wave past its region-B blocks; the next item's Q rows loaded in
+//      front of it): the item's rows are stored; the next item's region-B
+//      pieces are issued once its Q has arrived (the loop top).
+// The waits in front of B1 and S retire pieces issued half an item earlier; only
+// a workgroup's first item waits for its loads in the open.  Per-phase cycles:
+// ATT_STAMPS build, scripts/att_stamps.py.
 // ---------------------------------------------------------------------------
 // the lane id from an asm statement the compiler cannot hoist out of a loop
 __device__ __forceinline__ int lane_id_opaque()
@@ -349,6 +349,29 @@ __device__ __forceinline__ int lane_id_opaque()
     int l;
     asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
     return l;
+}
+
+// LDS-DMA issued from asm: hipcc's waitcnt pass cannot see it, so it no longer
+// puts a vmcnt(0) in front of the first LDS read after each issue (which retired
+// the next item's region-A prefetch in the first block after B1).  The kernel's
+// own waits in front of B1 and S are the only ones; no compiler-visible global
+// load may be in flight across the block loop's back edge (its wait there would
+// retire the hidden pieces too), and the compiler's waits for its own loads stay
+// conservative (hidden younger loads only make its vmcnt(N) stricter).
+__device__ __forceinline__ void glds16_hidden(const void *g, const void *lds)
+{
+    const uint32_t m = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char *)lds;
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m) : "memory", "m0");
+#pragma clang diagnostic pop
+}
+// every vector-memory op retired: the builtin for the compiler's own loads, the
+// asm copy for the hidden pieces
+__device__ __forceinline__ void wait_all_vm()
+{
+    wait_vmcnt<0>();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 #ifdef ATT_STAMPS
@@ -403,8 +426,8 @@ __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restr
             if (8 * i < nrows) {
                 const int row = 8 * i + (lane >> 3), pc = lane & 7;
                 const size_t so = (size_t)min(row, it.len - 1) * ld;
-                glds<16>(kbase + so + (pc ^ ((row >> 1) & 7)) * 8, Kl + i * 1024);
-                glds<16>(kbase + d + so + (pc ^ (((row >> 1) & 1) << 2)) * 8, Kl + LMAX * RB + i * 1024);
+                glds16_hidden(kbase + so + (pc ^ ((row >> 1) & 7)) * 8, Kl + i * 1024);
+                glds16_hidden(kbase + d + so + (pc ^ (((row >> 1) & 1) << 2)) * 8, Kl + LMAX * RB + i * 1024);
             }
         }
     };
@@ -551,13 +574,12 @@ __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restr
     int cur_i = blockIdx.x;
     if (cur_i >= n_items) return;                         // workgroup-uniform
     Item cur = item(cur_i);
-    // the first item: Q and region A in the open; region B under region A's
-    // blocks (retired by B1's wait, as in every later item)
+    // the first item: Q and region A in the open; region B (issued at the loop
+    // top) under region A's blocks, retired by B1's wait as in every later item
     load_q(cur);
     issue(cur, 0);
-    wait_vmcnt<0>();
+    wait_all_vm();
     __syncthreads();
-    issue(cur, 1);
     const h16 s16 = (h16)sl2;
     const h16x8 sc = {s16, s16, s16, s16, s16, s16, s16, s16};
 #ifdef ATT_STAMPS
@@ -575,6 +597,11 @@ __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restr
         // unconditional resets: nothing of the block state stays live across items
 #pragma unroll
         for (int st = 0; st < DH / 16; ++st) qf[st] *= sc;
+        // the item's region B, issued after the first use of Q (the compiler's
+        // wait for the Q loads retires every older piece); the empty asm keeps
+        // the issue below that wait
+        asm volatile("" ::"v"(qf[0]), "v"(qf[1]), "v"(qf[2]), "v"(qf[3]));
+        issue(cur, 1);
 #pragma unroll
         for (int t = 0; t < DH / 32; ++t)
 #pragma unroll
@@ -591,30 +618,31 @@ __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restr
             pv(0);
         }
         ASTAMP(1, __builtin_amdgcn_s_memtime());
-        bool qnext = false;
         // blocks 1-7 in one loop (one inlined copy of the block code), B1 at the
         // region boundary
 #pragma clang loop unroll(disable)
         for (int kb = 64; kb < LMAX; kb += 64) {
             if (kb == RH) {
                 ASTAMP(2, __builtin_amdgcn_s_memtime());
-                wait_vmcnt<0>();                          // this item's region-B pieces
+                wait_all_vm();                            // this item's region-B pieces
                 __syncthreads();                          // B1: region A is free
                 ASTAMP(3, __builtin_amdgcn_s_memtime());
                 if (more) issue(nx, 0);
             }
             if (active && kb < nrows) {
                 scores(kb);
-                if (more && kb >= RH && kb + 64 >= nrows) {
-                    load_q(nx);
-                    qnext = true;
-                }
                 pv(kb);
             }
         }
         ASTAMP(4, __builtin_amdgcn_s_memtime());
-        if (more && !qnext) load_q(nx);
-        wait_vmcnt<0>();                                  // the next item's region A and Q
+        // the next item's Q (the 4 youngest loads; none <=> no region-A pieces
+        // either), then every older piece: the next item's region A
+        if (more) {
+            load_q(nx);
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        } else {
+            wait_all_vm();
+        }
         __syncthreads();                                  // S: region B is free
         ASTAMP(5, __builtin_amdgcn_s_memtime());
         if (active) {
@@ -656,7 +684,6 @@ __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restr
         ++nit;
 #endif
         if (!more) break;
-        issue(nx, 1);
         cur = nx;
         cur_i = nx_i;
     }
