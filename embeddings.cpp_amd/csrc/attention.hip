@@ -462,7 +462,6 @@ __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restr
     int len = 0;                                          // the current item's
 
     auto qk = [&](int kb, bool bias) {
-        __builtin_amdgcn_s_setprio(1);
         int kbo[DH / 16];
 #pragma unroll
         for (int st = 0; st < DH / 16; ++st) {
@@ -483,7 +482,6 @@ __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restr
                 s[kh] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, qf[st], s[kh], 0, 0, 0);
             }
         }
-        __builtin_amdgcn_s_setprio(0);
         if (kb + 64 > len) {
 #pragma unroll
             for (int kh = 0; kh < 2; ++kh)
@@ -521,7 +519,6 @@ __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restr
         return rs;
     };
     auto pv = [&](int kb) {
-        __builtin_amdgcn_s_setprio(1);
         int vbo[DH / 32];
 #pragma unroll
         for (int t = 0; t < DH / 32; ++t) {
@@ -545,7 +542,6 @@ __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restr
                 }
             }
         }
-        __builtin_amdgcn_s_setprio(0);
     };
     // Q K^T and softmax of block kb > 0 (the first block, peeled off the block loop
     // sets the offset to its row max)
@@ -609,6 +605,7 @@ __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restr
         c = 0.f;
         l = 0.f;
         bbias[0] = zero;
+        __builtin_amdgcn_s_setprio(3);                    // block 0: see the block loop
         if (active) {                                     // block 0: the offset is its row max (f16-rounded)
             qk(0, false);
             c = (float)(h16)row_max();
@@ -628,6 +625,17 @@ __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restr
                 __syncthreads();                          // B1: region A is free
                 ASTAMP(3, __builtin_amdgcn_s_memtime());
                 if (more) issue(nx, 0);
+            }
+            // progress-based priority: the further a wave is past the last
+            // barrier, the lower its priority, so the 4 waves of a SIMD reach the
+            // next barrier together instead of in age order (the oldest wave of a
+            // SIMD ran its 4 blocks 2x faster than the youngest and then waited
+            // for it; 69.5 -> 65.8 us at C3, profiles/r02_att_stamps_prio.log)
+            switch ((kb >> 6) & 3) {
+            case 0: __builtin_amdgcn_s_setprio(3); break;
+            case 1: __builtin_amdgcn_s_setprio(2); break;
+            case 2: __builtin_amdgcn_s_setprio(1); break;
+            default: __builtin_amdgcn_s_setprio(0); break;
             }
             if (active && kb < nrows) {
                 scores(kb);

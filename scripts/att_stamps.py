@@ -14,7 +14,7 @@ import bertpy  # noqa: E402
 
 L = bertpy.load_lib(os.path.join(ROOT, "build", "stamps", "libbert.so"))
 us = ctypes.c_float()
-assert L.bertx_bench_attention(64, 512, 12, 64, 0, 20, ctypes.byref(us)) == 0
+assert L.bertx_bench_attention(64, 512, 12, 64, int(os.environ.get("ATT_VARIANT", "0")), 20, ctypes.byref(us)) == 0
 n = 1 << 17
 buf = (ctypes.c_ulonglong * n)()
 L.bertx_att_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
@@ -33,3 +33,13 @@ for it in range(3):
 span = (a[:, :, 2, 6].max(axis=1) - a[:, :, 0, 0].min(axis=1))
 print(f" workgroup span (3 items) median {np.median(span):.0f} cycles; implied clock {np.median(span) / (us.value * 1e3):.2f} GHz")
 # in-kernel wait of the first item's prologue: from the earliest item-0 start on a CU
+# per wave index: arrival at B1 and at S relative to the workgroup's item start
+print(" per wave (item 1): B1 arrival / S arrival after the item's first start, median over workgroups")
+x = a[:, :, 1, :]
+t0 = x[:, :, 0].min(axis=1, keepdims=True)
+b1 = np.median(x[:, :, 2] - t0, axis=0)
+sa = np.median(x[:, :, 4] - t0, axis=0)
+hw = x[:, :, 7]
+simd = (hw >> 4) & 3
+for w in range(16):
+    print(f"   wave {w:2d} simd {np.bincount(simd[:, w], minlength=4).argmax()}: B1 {b1[w]:7.0f}  S {sa[w]:7.0f}")
