@@ -1,7 +1,7 @@
 // Memory-bound row kernels: embeddings + LayerNorm, the LayerNorm statistics
 // of the residual stream, mean pool + L2 (the LN fold of kernels.h).
-// Embeddings: one wave per token row; each lane owns 4 consecutive features per
-// 256-wide slice (16-B loads and stores), reductions by wave shuffles.
+// Embeddings: one 16-lane group per token row; each lane owns 4 consecutive
+// features per 64-wide slice (16-B loads and stores), reductions by shuffles.
 #include "device_common.h"
 #include "host_common.h"
 #include "kernels.h"
@@ -12,7 +12,6 @@ namespace emb {
 
 namespace {
 
-constexpr int MAXV = 4;   // 4 slices x 256 features = n_embd <= 1024
 
 // 4 consecutive table values starting at column c (c % 4 == 0)
 __device__ __forceinline__ f32x4 table4(const DevTable &t, int row, int c)
@@ -51,52 +50,67 @@ __device__ __forceinline__ f32x4 table4(const DevTable &t, int row, int c)
     }
 }
 
+// One row per 16-lane group (4 rows per wave, 16 per block): each lane owns 4
+// consecutive features of every 64-wide slice, so all of a row's table loads are
+// in flight at once and the two reductions are 4 xor-shuffles each (a wave per
+// row with 64-lane reductions: 57 us at C3, latency-bound).
+constexpr int EMB_MAXS = 16;   // slices of 64 features: n_embd <= 1024
+
+__device__ __forceinline__ float sum16(float v)
+{
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
 __global__ __launch_bounds__(256) void embed_ln_kernel(DevTable word, DevTable type, DevTable pos,
                                                        const float *__restrict__ ln_w, const int32_t *__restrict__ ids,
                                                        const int32_t *__restrict__ cu, int d, h16 *__restrict__ z,
                                                        float2 *__restrict__ stats)
 {
-    const int b = blockIdx.y, lane = threadIdx.x & 63;
-    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int b = blockIdx.y, l16 = threadIdx.x & 15;
+    const int i = blockIdx.x * 16 + (threadIdx.x >> 4);
     const int start = cu[b], len = cu[b + 1] - start;
-    if (i >= len) return;
-    const int t = start + i, id = ids[t];
-    f32x4 v[MAXV];
+    const bool ok = i < len;                       // whole 16-lane groups: the shuffles stay in-group
+    const int t = start + (ok ? i : 0), id = ok ? ids[t] : 0;
+    const int ns = d / 64;
+    f32x4 v[EMB_MAXS];
     float s = 0.f;
 #pragma unroll
-    for (int k = 0; k < MAXV; ++k) {
-        const int c = 4 * (lane + 64 * k);
-        if (c < d) {
+    for (int k = 0; k < EMB_MAXS; ++k) {
+        if (k < ns) {
+            const int c = 4 * (l16 + 16 * k);
             // pos + (type[0] + word[id])  (bert.cpp:968-973 operand order), f32
-            const f32x4 w = table4(word, id, c), ty = table4(type, 0, c), p = table4(pos, i, c);
+            const f32x4 w = table4(word, id, c), ty = table4(type, 0, c), p = table4(pos, ok ? i : 0, c);
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[k][e] = p[e] + (ty[e] + w[e]);
             s += (v[k][0] + v[k][1]) + (v[k][2] + v[k][3]);
         }
     }
     // ggml_norm (eps 1e-5, mean then centred variance; bert.cpp:977-984) of the f32 row
-    const float mean = wave_sum(s) / (float)d;
+    const float mean = sum16(s) / (float)d;
     float s2 = 0.f;
 #pragma unroll
-    for (int k = 0; k < MAXV; ++k) {
-        const int c = 4 * (lane + 64 * k);
-        if (c < d) {
+    for (int k = 0; k < EMB_MAXS; ++k) {
+        if (k < ns) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) { const float u = v[k][e] - mean; s2 += u * u; }
         }
     }
-    const float r = 1.0f / sqrtf(wave_sum(s2) / (float)d + 1e-5f);
+    const float r = 1.0f / sqrtf(sum16(s2) / (float)d + 1e-5f);
+    if (!ok) return;
 #pragma unroll
-    for (int k = 0; k < MAXV; ++k) {
-        const int c = 4 * (lane + 64 * k);
-        if (c >= d) continue;
-        const f32x4 g = *(const f32x4 *)(ln_w + c);
-        h16x4 zh;
+    for (int k = 0; k < EMB_MAXS; ++k) {
+        if (k < ns) {
+            const int c = 4 * (l16 + 16 * k);
+            const f32x4 g = *(const f32x4 *)(ln_w + c);
+            h16x4 zh;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) zh[e] = (h16)(v[k][e] * g[e]);
-        *(h16x4 *)(z + (size_t)t * d + c) = zh;       // the stream as z = y * gamma (kernels.h LN fold)
+            for (int e = 0; e < 4; ++e) zh[e] = (h16)(v[k][e] * g[e]);
+            *(h16x4 *)(z + (size_t)t * d + c) = zh;   // the stream as z = y * gamma (kernels.h LN fold)
+        }
     }
-    if (lane == 0) stats[t] = float2{mean, r};
+    if (l16 == 0) stats[t] = float2{mean, r};
 }
 
 // Row statistics from the residual GEMM's 32-feature group partials (sum, M2 about
@@ -239,7 +253,7 @@ void launch_embed_ln(const DevTable &word, const DevTable &type, const DevTable 
                      const int32_t *ids, const int32_t *cu, int32_t n_seqs, int32_t max_len, int32_t d, uint16_t *z,
                      float2 *stats, hipStream_t s)
 {
-    dim3 grid((max_len + 3) / 4, n_seqs);
+    dim3 grid((max_len + 15) / 16, n_seqs);
     embed_ln_kernel<<<grid, 256, 0, s>>>(word, type, pos, ln_w, ids, cu, d, (h16 *)z, stats);
 }
 
