@@ -30,6 +30,7 @@
 #include "zregs.h"
 
 #include <cstdio>
+#include <algorithm>
 #include <cstdlib>
 #include <utility>
 
@@ -453,9 +454,18 @@ __global__ __launch_bounds__(64 * NW, 2) void gemmz_kernel(DevWeight W, const h1
                                                                int nN, int nTiles, LnFold ln)
 {
     __shared__ __attribute__((aligned(16))) char smem[NS * BM * ZK * 2 + zepi_lds<EPI, LNF, 32 * NW * FA, BM>()];
-    gemmz_body<FMT, EPI, LNF, NW, BM, NS, FA>(smem, blockIdx.x, W, X, bias, res, out, nN, nTiles, ln);
-    ZSTAMP(3, __builtin_amdgcn_s_memtime());
+    // a grid smaller than nTiles walks the tiles b, b + grid, ... (persistent;
+    // the host only launches it so when every wave of every tile has features,
+    // so no wave leaves the body early and the barrier between tiles is reached
+    // by all)
+    for (int b = blockIdx.x; b < nTiles; b += gridDim.x) {
+        gemmz_body<FMT, EPI, LNF, NW, BM, NS, FA>(smem, b, W, X, bias, res, out, nN, nTiles, ln);
+        ZSTAMP(3, __builtin_amdgcn_s_memtime());
+        if (b + (int)gridDim.x < nTiles) lds_barrier();   // LDS (X ring, epilogue operands) reused
+    }
 }
+
+int z_cus();
 
 template <int FMT, int NW, int BM, int NS, int FA = 1>
 void dispatch_z(const DevWeight &W, const h16 *x, int M, const float *bias, int epi, const void *res, void *out,
@@ -463,7 +473,18 @@ void dispatch_z(const DevWeight &W, const h16 *x, int M, const float *bias, int 
 {
     constexpr int BN = 32 * NW * FA;
     const int nN = (W.N + BN - 1) / BN, nTiles = (M / BM) * nN;
-    auto go = [&](auto kern) { kern<<<nTiles, 64 * NW, 0, s>>>(W, x, bias, res, out, nN, nTiles, ln); };
+    // Persistent when a launch is at most two rounds of two workgroups per CU
+    // (the N = d GEMMs at C3: 768 tiles = 1.5 rounds): 2 workgroups per CU walk
+    // the tiles, so a slot's second tile starts without a new dispatch (O-proj
+    // 53.7 -> 51.6 us, FFN-down 140.4 -> 136.6 us; the 4.5- and 6-round GEMMs
+    // measured 1-2 us slower so, profiles/r02_gemm_persist_ab.log).  Whole
+    // column tiles only.  BERT_GEMM_PERSIST = k forces k per CU, 0 = off.
+    static const int persist_env = [] { const char *e = std::getenv("BERT_GEMM_PERSIST"); return e ? std::atoi(e) : -1; }();
+    const int cus = z_cus();
+    const int persist = persist_env >= 0 ? persist_env : (nTiles <= 4 * cus ? 2 : 0);
+    int grid = nTiles;
+    if (persist > 0 && W.N % BN == 0) grid = std::min(nTiles, persist * cus);
+    auto go = [&](auto kern) { kern<<<grid, 64 * NW, 0, s>>>(W, x, bias, res, out, nN, nTiles, ln); };
     if (epi == EPI_BIAS_F16) {
         if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_F16, true, NW, BM, NS, FA>);
         else go(gemmz_kernel<FMT, EPI_BIAS_F16, false, NW, BM, NS, FA>);
