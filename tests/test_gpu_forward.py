@@ -137,6 +137,11 @@ def test_bge_base_q4_0_full_size(tmp_path):
     two = m.forward_batch(ids[:2])
     assert np.array_equal(two, full[:2])
     assert np.array_equal(m.forward_batch(ids[62:]), full[62:])
+    # every sentence bitwise as in 8-sentence batches (those launch one workgroup
+    # per tile; the full batch runs its N = 768 GEMMs persistent, the last half
+    # round as 128-row halves: gemm.hip gemmz_kernel)
+    eights = np.concatenate([m.forward_batch(ids[i:i + 8]) for i in range(0, 64, 8)])
+    assert np.array_equal(eights, full)
     ref = oracle_lib.Oracle(path).forward_batch([ids[0], ids[1], ids[63]], n_threads=min(16, os.cpu_count() or 1))
     assert np.all(cosines(full[[0, 1, 63]], ref) >= 1 - COS_TOL)
 
