@@ -146,6 +146,31 @@ __device__ __forceinline__ h16x4 lds_read_tr16(const void *p)
     return __builtin_bit_cast(h16x4, v);
 }
 
+// (mean, 1/sigma) of a row of d = 32 G features from its G 32-feature group
+// partials (sum, squared deviations about the group mean), Chan et al.:
+// mean = sum / d, M2 = sum_g M2_g + (s_g - 32 mean)^2 / 32; eps 1e-5
+// (ggml_norm, bert.cpp:1048-1056).  The arithmetic is pinned (explicit FMAs and
+// rounded ops, no contraction left to the compiler, groups added in index
+// order), so any other kernel that combines partials (the small-batch GEMM
+// prologue form of profiles/r02_stats_fold_small_ab.log) gives the same bits.
+template <int MAXG>
+__device__ __forceinline__ float2 ln_row_stats(const float2 (&p)[MAXG], int G, int d)
+{
+    float s = 0.f;
+#pragma unroll
+    for (int g = 0; g < MAXG; ++g)
+        if (g < G) s = __fadd_rn(s, p[g].x);
+    const float mean = __fdiv_rn(s, (float)d);
+    float m2 = 0.f;
+#pragma unroll
+    for (int g = 0; g < MAXG; ++g)
+        if (g < G) {
+            const float dm = fmaf(-32.0f, mean, p[g].x);
+            m2 = __fadd_rn(m2, fmaf(__fmul_rn(dm, dm), 1.0f / 32.0f, p[g].y));
+        }
+    return float2{mean, __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(__fdiv_rn(m2, (float)d), 1e-5f)))};
+}
+
 __device__ __forceinline__ void lds_barrier()
 {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

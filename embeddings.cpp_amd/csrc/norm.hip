@@ -123,16 +123,11 @@ __global__ __launch_bounds__(64) void ln_stats_any(const float2 *__restrict__ pa
 {
     const int t = blockIdx.x * 64 + threadIdx.x;
     if (t >= rows) return;
-    float s = 0.f;
-    for (int g = 0; g < G; ++g) s += part[(size_t)g * stride + t].x;
-    const float mean = s / (float)d;
-    float m2 = 0.f;
-    for (int g = 0; g < G; ++g) {
-        const float2 p = part[(size_t)g * stride + t];
-        const float dm = p.x - 32.0f * mean;
-        m2 += p.y + dm * dm * (1.0f / 32.0f);
-    }
-    stats[t] = float2{mean, 1.0f / sqrtf(m2 / (float)d + 1e-5f)};
+    float2 p[32];
+#pragma unroll
+    for (int g = 0; g < 32; ++g)
+        if (g < G) p[g] = part[(size_t)g * stride + t];
+    stats[t] = ln_row_stats<32>(p, G, d);
 }
 
 template <int G>
@@ -144,33 +139,24 @@ __global__ __launch_bounds__(64) void ln_stats_kernel(const float2 *__restrict__
     float2 p[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) p[g] = part[(size_t)g * stride + t];
-    float s = 0.f;
-#pragma unroll
-    for (int g = 0; g < G; ++g) s += p[g].x;
-    const float mean = s / (float)d;
-    float m2 = 0.f;
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        const float dm = p[g].x - 32.0f * mean;
-        m2 += p[g].y + dm * dm * (1.0f / 32.0f);
-    }
-    stats[t] = float2{mean, 1.0f / sqrtf(m2 / (float)d + 1e-5f)};
+    stats[t] = ln_row_stats<G>(p, G, d);
 }
 
 // pool stage 1: partial column sums of 64-token chunks, weights 1/len
 // (bert.cpp:1087-1089: sum_i X[i][c] * (1/len)).
 constexpr int POOL_CHUNK = 64;
 
-__global__ __launch_bounds__(256) void pool_partial_kernel(const h16 *__restrict__ z, const float2 *__restrict__ stats,
-                                                           const float *__restrict__ lw, const float *__restrict__ lb,
-                                                           const int32_t *__restrict__ cu, int d, int n_chunks,
-                                                           float *__restrict__ part)
+// Column sums of chunk ch of sentence b: thread t owns 8 columns (16-B loads)
+// of every TT-th token of the chunk: column group t % G (G = d / 8 <= 128),
+// token lane t / G; the token lanes are summed through LDS in a fixed order,
+// the result in (s0, s1) of threads t < G (columns 8t .. 8t + 7).
+__device__ __forceinline__ void pool_chunk_sum(const h16 *__restrict__ z, const float2 *__restrict__ stats,
+                                               const float *__restrict__ lw, const float *__restrict__ lb,
+                                               const int32_t *__restrict__ cu, int d, int b, int ch, f32x4 &s0,
+                                               f32x4 &s1)
 {
-    // thread t owns 8 columns (16-B loads) of every TT-th token of the chunk:
-    // column group t % G (G = d / 8 <= 128), token lane t / G; the token lanes
-    // are summed through LDS in a fixed order
     __shared__ f32x4 red[256][2];
-    const int b = blockIdx.y, ch = blockIdx.x, tid = threadIdx.x;
+    const int tid = threadIdx.x;
     const int start = cu[b], len = cu[b + 1] - start;
     const int i0 = ch * POOL_CHUNK, i1 = min(len, i0 + POOL_CHUNK);
     const int G = d / 8, TT = 256 / G, cg = tid % G, tl = tid / G;
@@ -197,29 +183,27 @@ __global__ __launch_bounds__(256) void pool_partial_kernel(const h16 *__restrict
     red[tid][1] = a1;
     __syncthreads();
     if (tid < G) {
-        f32x4 s0 = red[tid][0], s1 = red[tid][1];
+        s0 = red[tid][0];
+        s1 = red[tid][1];
         for (int k = 1; k < TT; ++k) {
             s0 += red[tid + k * G][0];
             s1 += red[tid + k * G][1];
         }
-        float *dst = part + ((size_t)b * n_chunks + ch) * d + 8 * tid;
-        *(f32x4 *)dst = s0;
-        *(f32x4 *)(dst + 4) = s1;
     }
 }
 
-// pool stage 2: sum the chunks, divide by the L2 norm (bert.cpp:1092-1095)
-__global__ __launch_bounds__(256) void pool_final_kernel(const float *__restrict__ part, int d, int n_chunks,
-                                                         float *__restrict__ out)
+// Sum the n_chunks column-sum rows of one sentence (part[k * d + c]) and
+// divide by the L2 norm (bert.cpp:1092-1095).
+__device__ __forceinline__ void pool_normalize(const float *part, int d, int n_chunks, float *__restrict__ out)
 {
     __shared__ float red[4];
-    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     float e[4];
     float ss = 0.f;
     int ne = 0;
     for (int c = tid; c < d; c += 256) {
         float v = 0.f;
-        for (int k = 0; k < n_chunks; ++k) v += part[((size_t)b * n_chunks + k) * d + c];
+        for (int k = 0; k < n_chunks; ++k) v += part[(size_t)k * d + c];
         e[ne++] = v;
         ss += v * v;
     }
@@ -228,7 +212,51 @@ __global__ __launch_bounds__(256) void pool_final_kernel(const float *__restrict
     __syncthreads();
     const float nrm = sqrtf((red[0] + red[1]) + (red[2] + red[3]));
     ne = 0;
-    for (int c = tid; c < d; c += 256) out[(size_t)b * d + c] = e[ne++] / nrm;
+    for (int c = tid; c < d; c += 256) out[c] = e[ne++] / nrm;
+}
+
+// pool stage 1: partial column sums of 64-token chunks, weights 1/len
+// (bert.cpp:1087-1089: sum_i X[i][c] * (1/len)).
+__global__ __launch_bounds__(256) void pool_partial_kernel(const h16 *__restrict__ z, const float2 *__restrict__ stats,
+                                                           const float *__restrict__ lw, const float *__restrict__ lb,
+                                                           const int32_t *__restrict__ cu, int d, int n_chunks,
+                                                           float *__restrict__ part)
+{
+    const int b = blockIdx.y, ch = blockIdx.x, tid = threadIdx.x;
+    f32x4 s0, s1;
+    pool_chunk_sum(z, stats, lw, lb, cu, d, b, ch, s0, s1);
+    if (tid < d / 8) {
+        float *dst = part + ((size_t)b * n_chunks + ch) * d + 8 * tid;
+        *(f32x4 *)dst = s0;
+        *(f32x4 *)(dst + 4) = s1;
+    }
+}
+
+// pool stage 2: sum the chunks, divide by the L2 norm
+__global__ __launch_bounds__(256) void pool_final_kernel(const float *__restrict__ part, int d, int n_chunks,
+                                                         float *__restrict__ out)
+{
+    const int b = blockIdx.x;
+    pool_normalize(part + (size_t)b * n_chunks * d, d, n_chunks, out + (size_t)b * d);
+}
+
+// Batches of at most one chunk (max_len <= 64): both stages in one launch, the
+// column sums through LDS instead of HBM, the same arithmetic as the two
+// kernels above (so the same bits).
+__global__ __launch_bounds__(256) void pool_one_kernel(const h16 *__restrict__ z, const float2 *__restrict__ stats,
+                                                       const float *__restrict__ lw, const float *__restrict__ lb,
+                                                       const int32_t *__restrict__ cu, int d, float *__restrict__ out)
+{
+    __shared__ __attribute__((aligned(16))) float cs[1024];
+    const int b = blockIdx.x, tid = threadIdx.x;
+    f32x4 s0, s1;
+    pool_chunk_sum(z, stats, lw, lb, cu, d, b, 0, s0, s1);
+    if (tid < d / 8) {
+        *(f32x4 *)(cs + 8 * tid) = s0;
+        *(f32x4 *)(cs + 8 * tid + 4) = s1;
+    }
+    __syncthreads();
+    pool_normalize(cs, d, 1, out + (size_t)b * d);
 }
 
 // diagnostics (BERT_CHECK_FINITE): count non-finite values of a buffer
@@ -268,7 +296,7 @@ void launch_ln_stats(const float2 *part, int32_t G, int32_t stride, int32_t rows
     case 24: ln_stats_kernel<24><<<nb, 64, 0, s>>>(part, stride, rows, d, stats); break;   // d 768
     case 32: ln_stats_kernel<32><<<nb, 64, 0, s>>>(part, stride, rows, d, stats); break;   // d 1024
     default:
-        // other widths (d % 64 == 0, d <= 1024): the same arithmetic, loads in a loop
+        // other widths (d % 64 == 0, d <= 1024): the same arithmetic (ln_row_stats)
         ln_stats_any<<<nb, 64, 0, s>>>(part, G, stride, rows, d, stats);
         break;
     }
@@ -280,6 +308,10 @@ void launch_pool_l2(const uint16_t *z, const float2 *stats, const float *ln_w, c
                     int32_t n_seqs, int32_t max_len, int32_t d, float *partial, float *out, hipStream_t s)
 {
     const int nc = pool_chunks(max_len);
+    if (nc == 1) {
+        pool_one_kernel<<<n_seqs, 256, 0, s>>>((const h16 *)z, stats, ln_w, ln_b, cu, d, out);
+        return;
+    }
     pool_partial_kernel<<<dim3(nc, n_seqs), 256, 0, s>>>((const h16 *)z, stats, ln_w, ln_b, cu, d, nc, partial);
     pool_final_kernel<<<n_seqs, 256, 0, s>>>(partial, d, nc, out);
 }
