@@ -1,10 +1,11 @@
 #!/bin/bash
-# A/B of the small-batch LN-statistics fold (BERT_STATS_FOLD_ROWS: default 4096
-# rows = fold, 0 = a statistics launch per sublayer as before): the GPU suite
-# once, then alternating bench runs whose probes (C2 f16 L128 B32, B 1 L 32
-# q4_0) are the small-batch workloads.  Every GPU step has its own limit.
+# A/B of a small-batch change against OFF_ENV (the environment that turns it
+# off; first used for the LN-statistics fold, BERT_STATS_FOLD_ROWS=0): the GPU
+# suite once, then alternating bench runs whose probes (C2 f16 L128 B32, B 1
+# L 32 q4_0) are the small-batch workloads.  Every GPU step has its own limit.
 set -o pipefail
 TAG=${TAG:-pfold}
+OFF_ENV=${OFF_ENV:-BERT_STATS_FOLD_ROWS=0}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
@@ -15,7 +16,7 @@ if [ "${SKIP_TESTS:-0}" != "1" ]; then
 fi
 for i in 1 2; do
   step 300 python bench.py --no-cpu-baseline --no-library > $OUT/bench_on$i.log 2>&1 || { tail -20 $OUT/bench_on$i.log; exit 1; }
-  BERT_STATS_FOLD_ROWS=0 step 300 python bench.py --no-cpu-baseline --no-library > $OUT/bench_off$i.log 2>&1 || { tail -20 $OUT/bench_off$i.log; exit 1; }
+  env $OFF_ENV timeout -k 10 300 python bench.py --no-cpu-baseline --no-library > $OUT/bench_off$i.log 2>&1 || { tail -20 $OUT/bench_off$i.log; exit 1; }
 done
 python3 - $OUT <<'P'
 import json, sys, glob, os
