@@ -14,7 +14,7 @@ if [ "${SKIP_TESTS:-0}" != "1" ]; then
   step 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests > $OUT/gputest.log 2>&1 || { tail -30 $OUT/gputest.log; exit 1; }
   tail -2 $OUT/gputest.log
 fi
-for i in 1 2; do
+for i in $(seq 1 ${ROUNDS:-2}); do
   step 300 python bench.py --no-cpu-baseline --no-library > $OUT/bench_on$i.log 2>&1 || { tail -20 $OUT/bench_on$i.log; exit 1; }
   env $OFF_ENV timeout -k 10 300 python bench.py --no-cpu-baseline --no-library > $OUT/bench_off$i.log 2>&1 || { tail -20 $OUT/bench_off$i.log; exit 1; }
 done
