@@ -262,6 +262,11 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     const int sw = (fr >> 1) & 7;
     const int rbase = fr << 7;
     int st = 0;
+#ifdef GEMM_STAMPS
+    // K-loop split (diagnostic): cycles in the load wait in front of each K-step's
+    // MFMAs, and in the wait + barrier behind them (slots 6, 7)
+    unsigned long long zw_front = 0, zw_back = 0;
+#endif
     // One K-step with CUR's weights: issue X(ks + NS - 1) into the stage freed by
     // the previous step and W(ks + 2) into the third register set, then an
     // explicit vmcnt equal to what is provably still in flight (a run-time no-op
@@ -279,16 +284,28 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
             wload(nxt2, k2);
             asm volatile("" ::: "memory");
             issue_x(kx, sx);
+#ifdef GEMM_STAMPS
+            const unsigned long long za = __builtin_amdgcn_s_memtime();
+#endif
             wait_vmcnt<2 * P + (NS == 4 ? XG : 0)>();
+#ifdef GEMM_STAMPS
+            zw_front += __builtin_amdgcn_s_memtime() - za;
+#endif
         }
         cur.pin_all();
         const uint32_t xs = lds_u32(smem + st * XB + rbase);
         zmma_items<NJ, FA, PF>(cur, xs + ((g ^ sw) << 4), xs + (((4 + g) ^ sw) << 4), acc,
                        std::make_integer_sequence<int, 2 * NJ>{});
+#ifdef GEMM_STAMPS
+        const unsigned long long zb = __builtin_amdgcn_s_memtime();
+#endif
         if constexpr (NS == 2) wait_vmcnt<LQ>();
         else if constexpr (NS == 3) wait_vmcnt<P>();
         else wait_vmcnt<P + XG>();
         lds_barrier();
+#ifdef GEMM_STAMPS
+        zw_back += __builtin_amdgcn_s_memtime() - zb;
+#endif
         st = st == NS - 1 ? 0 : st + 1;
     };
     int ks = 0;
@@ -306,7 +323,8 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
 #ifdef GEMM_STAMPS
     ZSTAMP(4, __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11)));
     ZSTAMP(5, __builtin_amdgcn_s_getreg((20) | (0 << 6) | (31 << 11)));
-    ZSTAMP(6, t);
+    ZSTAMP(6, zw_front);
+    ZSTAMP(7, zw_back);
 #endif
 
     // ---- epilogue ----

@@ -33,6 +33,9 @@ pro, kl, ep = a[:, 1] - a[:, 0], a[:, 2] - a[:, 1], a[:, 3] - a[:, 2]
 for nm, v in (("prologue", pro), ("K loop", kl), ("epilogue", ep), ("wave-tile", a[:, 3] - a[:, 0])):
     print(f"  {nm:9s} cycles: median {np.median(v):8.0f}  p10 {np.percentile(v, 10):8.0f}  p90 {np.percentile(v, 90):8.0f}")
 ksteps = K // 64
+# K-loop split (slots 6, 7; NS >= 3 forms): load wait in front of the MFMAs, wait + barrier behind them
+print(f"  K loop per K-step: front wait {np.median(a[:, 6]) / ksteps:.0f}, back wait + barrier {np.median(a[:, 7]) / ksteps:.0f}, "
+      f"rest (MFMA section) {np.median(kl - a[:, 6] - a[:, 7]) / ksteps:.0f} cycles")
 print(f"  K loop per K-step: {np.median(kl) / ksteps:.0f} cycles (MFMA floor per wave {64 * 16 * (bm // 256 if bm >= 256 else 1) * (2 if cfg == 5 else 1) * (bm // 128 if bm == 128 else 1) if False else 0})")
 # per CU: blocks (wave 0 rows) in start order
 cu = defaultdict(list)
