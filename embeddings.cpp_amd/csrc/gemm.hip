@@ -147,7 +147,7 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
 {
     constexpr int BN = 32 * NW * FA;
     constexpr int NJ = BM / 16;                 // 16-token B fragments per k-slice
-    constexpr int PF = FA == 1 ? 4 : 3;         // B-fragment read-ahead (items of 2 FA MFMAs)
+    constexpr int PF = FA == 1 ? (NJ <= 4 ? 2 * NJ - 1 : 4) : 3;   // B-fragment read-ahead (items of 2 FA MFMAs)
     constexpr int XB = BM * ZK * 2;             // bytes per X stage
     constexpr int XG = XB / (64 * NW * 16);     // LDS-DMA instructions per wave per stage
     constexpr int LQ = ZRegs<FMT>::LOADS * FA;
