@@ -13,11 +13,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "embeddings.cpp_amd"))
 import bertpy  # noqa: E402
 
-L = bertpy.load_lib(os.path.join(ROOT, "build", "stamps", "libbert.so"))
+L = bertpy.load_lib(os.environ.get("STAMPS_LIB", os.path.join(ROOT, "build", "stamps", "libbert.so")))
 N, K, epi, cfg = (int(x) for x in sys.argv[1:5])
 M = int(os.environ.get("SWEEP_M", "32768"))
 us = ctypes.c_float()
-rc = L.bertx_bench_gemm(2, N, K, M, epi, cfg, 1, ctypes.byref(us))
+rc = L.bertx_bench_gemm(int(os.environ.get("SWEEP_FMT", "2")), N, K, M, epi, cfg, 1, ctypes.byref(us))
 n = 1 << 18
 buf = (ctypes.c_ulonglong * n)()
 L.bertx_gemm_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
