@@ -13,10 +13,17 @@ there are no checkpoints offline.
 Prints ONE JSON line on rank 0.
 """
 import argparse
+import collections
+import csv
 import ctypes
+import glob
 import json
 import os
+import re
+import shutil
+import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -43,6 +50,8 @@ def parse():
     p.add_argument("--no-profile", action="store_true", help="disable live per-kernel event timing")
     p.add_argument("--no-probes", action="store_true", help="skip the north-star probes (C2 f16, B=1 L=32 q4_0)")
     p.add_argument("--no-library", action="store_true", help="skip the host-buffer library-path measurement")
+    p.add_argument("--no-pmc", action="store_true",
+                   help="skip this run's rocprofv3 PMC passes (HBM bytes per kernel launch, build/bin/bert_probe)")
     p.add_argument("--inproc", action="store_true",
                    help="one process drives --gpus GPUs through bert_forward_batch (the library's own sharding, "
                         "BERT_DEVICES=0..N-1) on --inproc-batch sentences of the --inproc-arch/--inproc-ftype model "
@@ -155,6 +164,93 @@ def dominant(stats):
     return dom["name"], dom["ms"] / dom["launches"] * 1e-3, dom["work"] / dom["launches"], dom["work_is_flops"]
 
 
+# --------------------------------------------------------------------------
+# this run's HBM counters (north_star: "rocprof reports achieved HBM GB/s")
+# --------------------------------------------------------------------------
+PROBE_BIN = os.path.join(ROOT, "build", "bin", "bert_probe")
+
+
+def kernel_class(name, state):
+    """bench kernel class of a rocprofv3 kernel name (mangled or demangled); the two
+    residual GEMMs of a layer (O-proj, FFN-down) share a form and alternate in
+    dispatch order (state counts them)."""
+    m = re.search(r"gemm[a-z0-9]*_kernelILi(\d+)ELi(\d+)E", name) or \
+        re.search(r"gemm[a-z0-9]*_kernel<(\d+), (\d+)", name)
+    if m:
+        epi = int(m.group(2))
+        if epi == 0:
+            return "gemm_qkv"
+        if epi == 1:
+            return "gemm_ffn_up"
+        state["res"] = state.get("res", 0) + 1
+        return "gemm_attn_out" if state["res"] % 2 == 1 else "gemm_ffn_down"
+    for key, cls in (("attention", "attention"), ("ln_stats", "ln_stats"), ("embed_ln", "embed_ln"),
+                     ("pool_", "pool_l2")):
+        if key in name:
+            return cls
+    return None
+
+
+def pmc_pass(model_path, B, L, counter, steps, warmup, timeout_s, device):
+    """One rocprofv3 counter pass over bert_probe (eager launches, so every kernel is
+    its own dispatch); returns [(class, KiB)] of the last `steps` forwards in dispatch
+    order, or raises."""
+    rp = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    out = tempfile.mkdtemp(prefix="bench_pmc_", dir="/tmp")
+    try:
+        env = dict(os.environ, BERT_GRAPHS="0", BERT_DEVICES=str(device), TMPDIR="/tmp")
+        cmd = ["timeout", "-s", "KILL", str(timeout_s), rp, "--pmc", counter, "--output-format", "csv",
+               "-d", out, "-o", "pmc", "--", PROBE_BIN, model_path, str(B), str(L), str(steps), str(warmup)]
+        r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                           timeout=timeout_s + 30)
+        if r.returncode != 0:
+            raise RuntimeError(f"rocprofv3 --pmc {counter} rc {r.returncode}: "
+                               + r.stdout.decode(errors="replace")[-300:])
+        files = glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)
+        if not files:
+            raise RuntimeError(f"no counter_collection.csv from rocprofv3 --pmc {counter}")
+        rows = [x for x in csv.DictReader(open(files[0])) if x["Counter_Name"] == counter]
+        rows.sort(key=lambda x: int(x["Dispatch_Id"]))
+        st, seq = {}, []
+        for x in rows:
+            c = kernel_class(x["Kernel_Name"], st)
+            if c:
+                seq.append((c, float(x["Counter_Value"])))
+        per_fwd = len(seq) // (steps + warmup)
+        if per_fwd == 0 or per_fwd * (steps + warmup) != len(seq):
+            raise RuntimeError(f"{len(seq)} kernel dispatches for {steps + warmup} forwards")
+        return seq[-steps * per_fwd:]
+    finally:
+        shutil.rmtree(out, ignore_errors=True)
+
+
+def pmc_live(model_path, B, L, device=0, steps=2, warmup=1, timeout_s=120):
+    """This run's HBM-side traffic of one forward of B x L tokens, per kernel class:
+    2 x FETCH_SIZE + WRITE_SIZE (KiB -> B; gfx950 FETCH_SIZE counts half the bytes of
+    16-B-per-lane reads, MI355X_MICROARCH.md "HBM"), from two rocprofv3 --pmc passes
+    (the two counters cannot share a pass) over build/bin/bert_probe.  Infinity-Cache
+    hits are included, so this is an upper bound on DRAM bytes."""
+    t0 = time.perf_counter()
+    fetch = pmc_pass(model_path, B, L, "FETCH_SIZE", steps, warmup, timeout_s, device)
+    write = pmc_pass(model_path, B, L, "WRITE_SIZE", steps, warmup, timeout_s, device)
+    agg = collections.defaultdict(lambda: [0.0, 0.0, 0])
+    for c, v in fetch:
+        agg[c][0] += 2.0 * v * 1024 / steps
+        agg[c][2] += 1
+    for c, v in write:
+        agg[c][1] += v * 1024 / steps
+    per_class = {}
+    for c, (fb, wb, n) in sorted(agg.items()):
+        launches = n / steps
+        per_class[c] = {"launches_per_forward": launches, "bytes_per_launch": int((fb + wb) / launches),
+                        "fetch_bytes_per_forward": int(fb), "write_bytes_per_forward": int(wb)}
+    total = int(sum(v[0] + v[1] for v in agg.values()))
+    return {"bytes_per_forward": total, "per_class": per_class, "forwards_counted": steps,
+            "source": "this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over build/bin/bert_probe "
+                      "(eager launches of the same kernels), 2 x FETCH_SIZE + WRITE_SIZE per MI355X_MICROARCH.md",
+            "pmc_seconds": round(time.perf_counter() - t0, 1)}
+
+
 def probes(lib, bertpy, torch, a, dev, stream, q4_path):
     """BASELINE.json north_star: 'rocprof reports achieved HBM GB/s on the q4_0 path and
     MFMA utilisation on the f16 path against gfx950 peak'.  Two probes, each timed
@@ -163,8 +259,9 @@ def probes(lib, bertpy, torch, a, dev, stream, q4_path):
         dominant kernel's achieved TFLOP/s against the 2.5 PF dense f16 peak;
       q4_0_hbm: bge-base q4_0, B 1, L 32 (SURVEY §8d's bandwidth-bound probe, AI ~40)
         -- forward latency and algorithmic bytes (weights at stored width + rows +
-        ids + output) / latency against 8 TB/s.  PMC traffic of the same run:
-        profiles/r02_probe_q4_0_b1_pmc.json."""
+        ids + output) / latency against 8 TB/s, and this run's counter bytes (pmc_live)
+        / latency beside it.  The probe always builds bge-base-en-v1.5 q4_0, whatever
+        --arch/--ftype the headline runs."""
     out = {}
     steps = max(a.steps, 20)
     # C2
@@ -187,9 +284,17 @@ def probes(lib, bertpy, torch, a, dev, stream, q4_path):
                        "step_tflops": round(32 * flop_per_sentence(hp, 128) * steps / el / 1e12, 1),
                        "kernel_avg_us": {s["name"]: round(s["ms"] * 1e3 / s["launches"], 2)
                                          for s in st if s["launches"]}}
+    if not a.no_pmc:
+        try:
+            pm = pmc_live(p2, 32, 128, device=int(os.environ.get("LOCAL_RANK", "0")))
+            pm["gbps_at_measured_step"] = round(pm["bytes_per_forward"] / (el / steps) / 1e9, 1)
+            out["f16_mfma"]["pmc"] = pm
+        except Exception as ex:   # a report, never the metric
+            out["f16_mfma"]["pmc"] = {"error": str(ex)}
     del f
     # bandwidth probe: bge-base q4_0, one sentence of 32 tokens
     hp = bertpy.ARCHS["bge-base-en-v1.5"]
+    q4_path = ensure_model(bertpy, a.model_dir, "bge-base-en-v1.5", "q4_0", a.seed)
     f = DeviceForward(lib, bertpy, torch, q4_path, bertpy.synthetic_ids(1, 32, hp["n_vocab"], seed=7), dev, stream)
     for _ in range(3):
         f.step()
@@ -209,13 +314,14 @@ def probes(lib, bertpy, torch, a, dev, stream, q4_path):
                        "kernels_per_forward": launches, "sum_kernel_us": round(kern_s * 1e6, 1),
                        "kernel_avg_us": {s["name"]: round(s["ms"] * 1e3 / s["launches"], 2)
                                          for s in st if s["launches"]}}
-    pmc = os.path.join(ROOT, "profiles", "r02_probe_q4_0_b1_pmc.json")
-    if os.path.exists(pmc):
+    if not a.no_pmc:
         try:
-            with open(pmc) as fh:
-                out["q4_0_hbm"]["pmc"] = json.load(fh)
-        except Exception:
-            pass
+            pm = pmc_live(q4_path, 1, 32, device=int(os.environ.get("LOCAL_RANK", "0")), steps=3)
+            gbps = pm["bytes_per_forward"] / lat / 1e9
+            pm.update({"counter_gbps": round(gbps, 2), "counter_hbm_frac": round(gbps / HBM_PEAK_GBPS, 5)})
+            out["q4_0_hbm"]["pmc"] = pm
+        except Exception as ex:
+            out["q4_0_hbm"]["pmc"] = {"error": str(ex)}
     del f
     return out
 
@@ -364,15 +470,30 @@ def main():
                 ach = per_launch / avg_s / 1e9
                 roofline = {"kernel": dom["name"], "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS,
                             "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None}
-        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if roofline and os.path.exists(pmc):
-            try:
-                with open(pmc) as f:
-                    tr = json.load(f).get(roofline["kernel"])
-                if tr is not None:
-                    roofline["traffic"] = tr
-            except Exception:
-                pass
+
+    # this run's HBM counters for the headline workload (rank 0 of a single-process
+    # run: two rocprofv3 --pmc passes over build/bin/bert_probe on the same model)
+    pm = None
+    if rank == 0 and world == 1 and not a.no_pmc:
+        try:
+            pm = pmc_live(path, B, L, device=local)
+        except Exception as ex:   # a report, never the metric
+            pm = {"error": str(ex)}
+    if roofline:
+        if pm and "per_class" in pm and roofline["kernel"] in pm["per_class"]:
+            roofline["traffic"] = pm["per_class"][roofline["kernel"]]["bytes_per_launch"]
+            roofline["traffic_source"] = "this run (rocprofv3 PMC, 2 x FETCH_SIZE + WRITE_SIZE per launch)"
+        else:
+            rec = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+            if os.path.exists(rec):
+                try:
+                    with open(rec) as f:
+                        tr = json.load(f).get(roofline["kernel"])
+                    if tr is not None:
+                        roofline["traffic"] = tr
+                        roofline["traffic_source"] = "recorded: profiles/pmc_traffic.json (an earlier PMC session)"
+                except Exception:
+                    pass
 
     alg_bytes = algorithmic_bytes(hp, a.ftype, B, L)
     res = {
@@ -394,23 +515,16 @@ def main():
         "roofline": roofline,
         "kernels": kernels,
     }
-    # measured HBM traffic of the step: per-launch FETCH/WRITE bytes of each kernel
-    # class (rocprofv3 PMC passes of this bench, profiles/pmc_traffic.json) x launches
-    # per step, over the graph-replayed step time
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if stats and os.path.exists(pmc) and not (a.arch != "bge-base-en-v1.5" or a.ftype != "q4_0" or B != 64 or L != 512):
-        try:
-            with open(pmc) as f:
-                tr = json.load(f)
-            per_step = sum(tr[s_["name"]] * s_["launches"] / a.steps for s_ in stats
-                           if s_["launches"] and s_["name"] in tr)
-            res["hbm"] = {"bytes_per_step": int(per_step), "gbps": round(per_step / (ms_per_step * 1e-3) / 1e9, 1),
-                          "peak_gbps": HBM_PEAK_GBPS,
-                          "frac": round(per_step / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
-                          "source": "profiles/pmc_traffic.json (2 x FETCH_SIZE + WRITE_SIZE per launch, "
-                                    "MI355X_MICROARCH.md gfx950 correction) x launches per step / step time"}
-        except Exception as ex:   # a report, never the metric
-            res["hbm"] = {"error": str(ex)}
+    # measured HBM traffic of the step: this run's PMC bytes of one forward over the
+    # graph-replayed step time
+    if pm is not None:
+        if "bytes_per_forward" in pm:
+            gb = pm["bytes_per_forward"] / (ms_per_step * 1e-3) / 1e9
+            res["hbm"] = {"bytes_per_step": pm["bytes_per_forward"], "gbps": round(gb, 1), "peak_gbps": HBM_PEAK_GBPS,
+                          "frac": round(gb / HBM_PEAK_GBPS, 4), "per_class": pm["per_class"], "source": pm["source"],
+                          "pmc_seconds": pm["pmc_seconds"]}
+        else:
+            res["hbm"] = pm
     if lib_el is not None:
         res["library_path"] = {"value": round(B * world * a.steps / lib_el, 2), "unit": "sentences/s",
                                "ms_per_step": round(lib_el / a.steps * 1e3, 4),

@@ -293,13 +293,18 @@ def synthetic_tensors(hp, seed=1234, profile="survey"):
     three residual outlier channels (`outlier_channels`) the way trained BERT/BGE
     checkpoints have them: O-proj and FFN-down biases of +-30/60/90 there with LN
     gains of 0.3, so the pre-LN (f16) residual stream reaches |x| ~ 100 on those
-    channels while they do not swamp the LayerNorm."""
+    channels while they do not swamp the LayerNorm.
+
+    profile "sharp_mean": "sharp" plus a constant +16 on every channel of the
+    O-proj and FFN-down biases, so every pre-LN residual row carries a mean of
+    ~16 against a spread of a few units (the regime where the LN fold's
+    z = f16(y * gamma) rounds with |y| rather than |y - mean|)."""
     rng = np.random.default_rng(seed)
     d, f = hp["n_embd"], hp["n_intermediate"]
     shapes = {"word": (hp["n_vocab"], d), "pos": (hp["n_max_tokens"], d), "type": (2, d), "dd": (d, d),
               "fd": (f, d), "df": (d, f), "d": (d,), "f": (f,), "ln_w": (d,), "ln_b": (d,)}
-    sharp = profile == "sharp"
-    assert profile in ("survey", "sharp"), profile
+    sharp = profile in ("sharp", "sharp_mean")
+    assert profile in ("survey", "sharp", "sharp_mean"), profile
     oc = outlier_channels(d, seed) if sharp else None
     # Q/K spread: 24 layers of peaked attention amplify the reference's own q8
     # activation rounding (bge-large at 0.05: oracle vs the same oracle with f32
@@ -321,6 +326,8 @@ def synthetic_tensors(hp, seed=1234, profile="survey"):
                 a += np.float32(1.0)
         if sharp and role == "d" and name.endswith("output.dense.bias"):
             a[oc] += np.float32([30.0, -60.0, 90.0]) * np.float32(min(1.0, d / 768))
+            if profile == "sharp_mean":
+                a += np.float32(16.0)
         out[name] = a
     return out
 

@@ -697,20 +697,7 @@ __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restr
     }
 }
 
-// CUs of the current device (persistent grids)
-static int att_cus()
-{
-    static const int n = [] {
-        int dev = 0, cus = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-            cus = 256;
-        return cus;
-    }();
-    return n;
-}
-
-int g_att_variant = 0;   // benches only (bertx_bench_attention)
+thread_local int g_att_variant = 0;   // benches only (bertx_bench_attention), per calling thread
 
 void launch_attention(const uint16_t *qkv, const int32_t *cu, int32_t n_seqs, int32_t max_len, int32_t n_head,
                       int32_t d, uint16_t *out, hipStream_t s)
@@ -723,7 +710,7 @@ void launch_attention(const uint16_t *qkv, const int32_t *cu, int32_t n_seqs, in
             // 0: production (attention_lds3, persistent, one workgroup per CU); 7:
             // the same kernel on at most 7 workgroups (tests: many ragged items each)
             const int n_items = n_seqs * n_head;
-            const int cap = g_att_variant == 7 ? 7 : att_cus();
+            const int cap = g_att_variant == 7 ? 7 : device_cu_count();
             const int grid = n_items < cap ? n_items : cap;
             if (grid > 0)
                 attention_lds3_kernel<<<grid, 1024, 0, s>>>((const h16 *)qkv, cu, d, n_head, n_items, sl2, (h16 *)out);

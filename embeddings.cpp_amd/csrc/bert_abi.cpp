@@ -130,7 +130,12 @@ int run_forward(bert_ctx *ctx, const int32_t *const *toks, const int32_t *lens, 
         for (auto &t : th) t.join();
     }
     for (int dv = 0; dv < nd; ++dv)
-        if (assign[(size_t)dv].empty()) ctx->devices[(size_t)dv]->set_last_call(0.0, 0, 0);
+        if (assign[(size_t)dv].empty()) {
+            // under the replica's mutex, like the busy replicas' stamps (bertx_device_last_call reads them)
+            Device &D = *ctx->devices[(size_t)dv];
+            std::lock_guard<std::mutex> lk(D.mutex());
+            D.set_last_call(0.0, 0, 0);
+        }
     for (int rc : rcs) if (rc != 0) {
         std::fprintf(stderr, "libbert: forward failed (%d)\n", rc);
         return rc;
@@ -403,7 +408,8 @@ int32_t bertx_device_last_call(struct bert_ctx *ctx, int32_t slot, double *wall_
                                int64_t *n_tokens)
 {
     if (!ctx || slot < 0 || slot >= (int32_t)ctx->devices.size()) return -1;
-    const Device &D = *ctx->devices[(size_t)slot];
+    Device &D = *ctx->devices[(size_t)slot];
+    std::lock_guard<std::mutex> lk(D.mutex());   // the stamps are written under it (run_forward)
     if (wall_ms) *wall_ms = D.last_call_ms();
     if (n_seqs) *n_seqs = D.last_call_seqs();
     if (n_tokens) *n_tokens = D.last_call_tokens();

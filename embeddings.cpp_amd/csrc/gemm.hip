@@ -33,6 +33,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <utility>
+#include <atomic>
 
 namespace emb {
 
@@ -483,8 +484,6 @@ __global__ __launch_bounds__(64 * NW, 2) void gemmz_kernel(DevWeight W, const h1
     }
 }
 
-int z_cus();
-
 template <int FMT, int NW, int BM, int NS, int FA = 1>
 void dispatch_z(const DevWeight &W, const h16 *x, int M, const float *bias, int epi, const void *res, void *out,
                 hipStream_t s, const LnFold &ln, bool lnf)
@@ -498,7 +497,7 @@ void dispatch_z(const DevWeight &W, const h16 *x, int M, const float *bias, int 
     // measured 1-2 us slower so, profiles/r02_gemm_persist_ab.log).  Whole
     // column tiles only.  BERT_GEMM_PERSIST = k forces k per CU, 0 = off.
     static const int persist_env = [] { const char *e = std::getenv("BERT_GEMM_PERSIST"); return e ? std::atoi(e) : -1; }();
-    const int cus = z_cus();
+    const int cus = device_cu_count();
     const int persist = persist_env >= 0 ? persist_env : (nTiles <= 4 * cus ? 2 : 0);
     int grid = nTiles;
     if (persist > 0 && W.N % BN == 0) grid = std::min(nTiles, persist * cus);
@@ -515,19 +514,6 @@ void dispatch_z(const DevWeight &W, const h16 *x, int M, const float *bias, int 
     }
 }
 
-// CUs of the current device.
-int z_cus()
-{
-    static const int cus = [] {
-        int dev = 0, n = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-            n = 256;
-        return n;
-    }();
-    return cus;
-}
-
 template <int FMT>
 void launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, int32_t epi, const void *res,
                 void *out, hipStream_t s, const LnFold &ln, bool lnf, int cfg)
@@ -536,7 +522,7 @@ void launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, 
         // the largest tile that still gives every CU work: 256 x 128 tiles two per CU
         // (measured fastest at C3 once there are two per CU, profiles/r01_gemm16_sweep.log),
         // else 128 x 128 once there is one per CU, else 64 x 64 (small batches)
-        const long n128 = (W.N + 127) / 128, cus = z_cus();
+        const long n128 = (W.N + 127) / 128, cus = device_cu_count();
         cfg = (M % 256 == 0 && (M / 256) * n128 >= 2 * cus) ? 2 : (M % 128 == 0 && (M / 128) * n128 >= cus) ? 3 : 4;
     }
     if (cfg == 2 && M % 256 == 0) dispatch_z<FMT, 4, 256, 2>(W, x, M, bias, epi, res, out, s, ln, lnf);
@@ -547,7 +533,25 @@ void launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, 
 
 }  // namespace
 
-int g_gemm_cfg = 0;
+thread_local int g_gemm_cfg = 0;
+
+// CUs of the calling thread's current device, cached per ordinal (a context may
+// hold devices in different partition modes; launches size persistent grids
+// and tile configs by the device they run on)
+int device_cu_count()
+{
+    static std::atomic<int> cache[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0) { (void)hipGetLastError(); return 256; }
+    if (dev < 64) {
+        const int c = cache[dev].load(std::memory_order_relaxed);
+        if (c > 0) return c;
+    }
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    if (dev < 64) cache[dev].store(n, std::memory_order_relaxed);
+    return n;
+}
 
 #ifdef GEMM_STAMPS
 extern "C" __attribute__((visibility("default"))) int bertx_gemm_stamps(unsigned long long *host, size_t n)

@@ -93,7 +93,11 @@ int launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *b
                 const void *res, void *out, hipStream_t s, const LnFold &ln = LnFold());
 // Tests/benches: tile config (0 = heuristic, 2 = 4 waves 256x128, 3 = 4 waves 128x128,
 // 4 = 2 waves 64x64).
-extern int g_gemm_cfg;
+// Per calling thread, so a test hook never changes a forward running on another thread.
+extern thread_local int g_gemm_cfg;
+
+// CU count of the calling thread's current HIP device (cached per ordinal).
+int device_cu_count();
 
 // z = f16((pos[i] + (type[0] + word[id])) * gamma) and the (mean, 1/sigma) of
 // the f32 sum, for every valid token (bert.cpp:963-984).
@@ -103,11 +107,12 @@ void launch_embed_ln(const DevTable &word, const DevTable &type, const DevTable 
 
 // stats[t] = (mean, 1/sqrt(var + 1e-5)) of rows t < rows from the G = d/32 group
 // partials part[g * stride + t] a residual GEMM wrote (ggml_norm, bert.cpp:1048-1056).
-void launch_ln_stats(const float2 *part, int32_t G, int32_t stride, int32_t rows, int32_t d, float2 *stats,
+// Returns -1 (nothing launched) unless d == 32 G with G <= 32.
+int launch_ln_stats(const float2 *part, int32_t G, int32_t stride, int32_t rows, int32_t d, float2 *stats,
                      hipStream_t s);
 
 // Benches only: attention kernel variant (bertx_bench_attention).
-extern int g_att_variant;
+extern thread_local int g_att_variant;
 
 // Per (sentence, head) softmax(Q K^T / sqrt(dh)) V over the sentence's own keys.
 void launch_attention(const uint16_t *qkv, const int32_t *cu, int32_t n_seqs, int32_t max_len, int32_t n_head,

@@ -285,10 +285,13 @@ void launch_embed_ln(const DevTable &word, const DevTable &type, const DevTable 
     embed_ln_kernel<<<grid, 256, 0, s>>>(word, type, pos, ln_w, ids, cu, d, (h16 *)z, stats);
 }
 
-void launch_ln_stats(const float2 *part, int32_t G, int32_t stride, int32_t rows, int32_t d, float2 *stats,
-                     hipStream_t s)
+int launch_ln_stats(const float2 *part, int32_t G, int32_t stride, int32_t rows, int32_t d, float2 *stats,
+                    hipStream_t s)
 {
-    if (rows <= 0) return;
+    // the kernels hold at most 32 partials per row (d <= 1024): a wider row would
+    // silently drop groups, so it is refused
+    if (G <= 0 || G > 32 || d != 32 * G) return -1;
+    if (rows <= 0) return 0;
     const int nb = (rows + 63) / 64;
     switch (G) {
     case 12: ln_stats_kernel<12><<<nb, 64, 0, s>>>(part, stride, rows, d, stats); break;   // d 384
@@ -300,6 +303,7 @@ void launch_ln_stats(const float2 *part, int32_t G, int32_t stride, int32_t rows
         ln_stats_any<<<nb, 64, 0, s>>>(part, G, stride, rows, d, stats);
         break;
     }
+    return 0;
 }
 
 int32_t pool_chunks(int32_t max_len) { return (max_len + POOL_CHUNK - 1) / POOL_CHUNK; }

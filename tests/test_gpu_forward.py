@@ -138,8 +138,8 @@ def test_bge_base_q4_0_full_size(tmp_path):
     assert np.array_equal(two, full[:2])
     assert np.array_equal(m.forward_batch(ids[62:]), full[62:])
     # every sentence bitwise as in 8-sentence batches (those launch one workgroup
-    # per tile; the full batch runs its N = 768 GEMMs persistent, the last half
-    # round as 128-row halves: gemm.hip gemmz_kernel)
+    # per tile; the full batch runs its N = 768 GEMMs persistent, two workgroups
+    # per CU walking the tiles: gemm.hip dispatch_z)
     eights = np.concatenate([m.forward_batch(ids[i:i + 8]) for i in range(0, 64, 8)])
     assert np.array_equal(eights, full)
     ref = oracle_lib.Oracle(path).forward_batch([ids[0], ids[1], ids[63]], n_threads=min(16, os.cpu_count() or 1))
@@ -275,3 +275,62 @@ def test_device_forward_on_caller_stream_is_ordered_before_host_forward(quant_mo
     for p in (d_ids, d_cu, d_out):
         hip.hipFree(p)
     hip.hipStreamDestroy(s)
+
+
+@pytest.fixture(scope="module")
+def c4_model(tmp_path_factory):
+    p = str(tmp_path_factory.mktemp("c4") / "bge-large-en-v1.5-q4_1.bin")
+    bertpy.synthetic_model(p, "bge-large-en-v1.5", "q4_1", seed=1234)
+    return p
+
+
+def _replicas(path, n, monkeypatch):
+    monkeypatch.setenv("BERT_DEVICES", ",".join(["0"] * n))
+    m = bertpy.BertModel(path)
+    assert m.lib.bertx_num_devices(m.ctx) == n
+    return m
+
+
+def test_c4_256_sentences_over_8_replicas(c4_model, monkeypatch):
+    """SURVEY §8 C4 as specified: bge-large q4_1, L 512, 256 sentences through
+    bert_forward_batch (reference entry bert.cpp:1374-1444) split by the library over
+    8 replicas (BERT_DEVICES=0 x 8: 8 weight replicas, host threads, streams and
+    workspaces on the one GPU, the code path an 8-GPU node takes).  32 sentences per
+    slot, bitwise equal to one replica, 8 sentences against the oracle."""
+    hp = bertpy.ARCHS["bge-large-en-v1.5"]
+    ids = bertpy.synthetic_ids(256, 512, hp["n_vocab"], seed=7)
+    one = bertpy.BertModel(c4_model).forward_batch(ids)
+    assert np.all(np.isfinite(one))
+    m8 = _replicas(c4_model, 8, monkeypatch)
+    eight = m8.forward_batch(ids)
+    per = m8.device_last_call()
+    assert [p[1] for p in per] == [32] * 8, per
+    assert [p[2] for p in per] == [32 * 512] * 8, per
+    assert np.array_equal(eight, one)
+    check = [0, 31, 32, 100, 128, 200, 254, 255]
+    ref = oracle_lib.Oracle(c4_model).forward_batch([ids[i] for i in check], n_threads=min(16, os.cpu_count() or 1))
+    c = cosines(eight[check], ref)
+    print("C4 over 8 replicas: min cos vs oracle", c.min())
+    assert np.all(c >= 1 - COS_TOL), c
+
+
+def test_c5_ragged_over_8_replicas(tmp_path, monkeypatch):
+    """C5 (bge-base-zh q8_0, ragged 16..512, 128 sentences) over 8 replicas: the
+    FLOP-cost split (longest-first to the least-loaded replica) gives the replicas
+    unequal token counts and different sentence lengths; every sentence is still
+    bitwise as on one replica."""
+    hp = bertpy.ARCHS["bge-base-zh-v1.5"]
+    path = str(tmp_path / "bge-base-zh-q8_0.bin")
+    bertpy.synthetic_model(path, "bge-base-zh-v1.5", "q8_0", seed=1234)
+    lens = [int(x) for x in np.random.default_rng(11).integers(16, 513, 128)]
+    ids = bertpy.synthetic_ids(128, lens, hp["n_vocab"], seed=7)
+    one = bertpy.BertModel(path).forward_batch(ids)
+    m8 = _replicas(path, 8, monkeypatch)
+    eight = m8.forward_batch(ids)
+    per = m8.device_last_call()
+    counts = [p[1] for p in per]
+    assert sum(counts) == 128 and all(c > 0 for c in counts), per
+    toks = [p[2] for p in per]
+    assert sum(toks) == sum(lens) and len(set(toks)) > 1, per   # ragged shards
+    assert max(p[0] for p in per) > 0.0
+    assert np.array_equal(eight, one)
