@@ -82,6 +82,8 @@ def load_lib(path=None):
     L.bertx_test_gemm.argtypes = [c_i32, c_i32, c_i32, vp, c_f32p, c_i32, vp, c_i32, vp, vp, c_i32]
     L.bertx_test_gemm_ln.restype = c_i32
     L.bertx_test_gemm_ln.argtypes = [c_i32, c_i32, c_i32, vp, vp, c_i32, vp, vp, vp, vp, c_i32] + [vp] * 7 + [c_i32]
+    L.bertx_test_gemm_f32.restype = c_i32
+    L.bertx_test_gemm_f32.argtypes = [c_i32, c_i32, vp, vp, c_i32, vp, c_i32, vp, vp]
     L.bertx_bench_gemm.restype = c_i32
     L.bertx_bench_gemm.argtypes = [c_i32] * 7 + [c_f32p]
     L.bertx_bench_attention.restype = c_i32

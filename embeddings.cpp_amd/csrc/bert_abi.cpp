@@ -233,8 +233,8 @@ struct bert_ctx *bert_load_from_file(const char *fname)
     }
     std::printf("bert_load_from_file: MI355X engine on %zu HIP device(s)\n", ctx->devices.size());
     if (m.hp.ftype == emb::FMT_F32)
-        std::printf("bert_load_from_file: f32 file: linear weights run as f16 MFMA operands with f32 accumulation "
-                    "(the reference multiplies f32 x f32, bert.cpp:499-503)\n");
+        std::printf("bert_load_from_file: f32 file: f32 activations x f32 weights on the f32 MFMA chain "
+                    "(as the reference multiplies them, bert.cpp:499-503)\n");
     return ctx.release();
 }
 

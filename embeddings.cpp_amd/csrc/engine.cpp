@@ -264,8 +264,10 @@ void Device::upload(const HostModel &m)
                      d, f, d / hp_.n_head);
         return;
     }
-    // f32 files keep f32-accurate weights as f16 hi/lo pairs (repack_linear_f32)
     wfmt_ = hp_.ftype;
+    // f32 files run the f32 chain (f32.hip) on the file's own f32 rows; the other
+    // formats the lane-order layout of the MFMA f16 GEMMs
+    f32_ = wfmt_ == FMT_F32;
     std::vector<Piece> pieces;
     pieces.reserve(16 + 24 * (size_t)hp_.n_layer);
     auto add = [&](Piece &&p) -> size_t { pieces.push_back(std::move(p)); return pieces.size() - 1; };
@@ -295,11 +297,35 @@ void Device::upload(const HostModel &m)
         i1 = add(std::move(c1));
         i2 = add(std::move(c2));
     };
-    struct LIdx { LinIdx qkv, o, up, down; size_t bo, bdown, c1q, c2q, c1u, c2u, l1w, l1b, l2w, l2b; };
+    // f32 chain: the rows of the parts as f32 (concatenated along N)
+    auto rows32 = [&](std::vector<const HostTensor *> parts) -> size_t {
+        Piece p;
+        for (const HostTensor *t : parts) {
+            const size_t n0 = p.bytes.size();
+            p.bytes.resize(n0 + (size_t)t->ne1 * t->ne0 * 4);
+            for (int r = 0; r < t->ne1; ++r)
+                dequant_row(t->fmt, t->bytes.data() + fmt_row_bytes(t->fmt, t->ne0) * r,
+                            (float *)(p.bytes.data() + n0) + (size_t)r * t->ne0, t->ne0);
+        }
+        return add(std::move(p));
+    };
+    struct LIdx {
+        LinIdx qkv, o, up, down;
+        size_t bo, bdown, c1q, c2q, c1u, c2u, l1w, l1b, l2w, l2b;
+        size_t w32q, w32o, w32u, w32d, bq, bu;
+    };
     std::vector<LIdx> li((size_t)hp_.n_layer);
     for (int l = 0; l < hp_.n_layer; ++l) {
         const HostLayer &L = m.layers[(size_t)l];
         LIdx &x = li[(size_t)l];
+        if (f32_) {
+            x.w32q = rows32({&L.q_w, &L.k_w, &L.v_w}); x.w32o = rows32({&L.o_w});
+            x.w32u = rows32({&L.i_w}); x.w32d = rows32({&L.o2_w});
+            x.bq = rows32({&L.q_b, &L.k_b, &L.v_b}); x.bu = vec(L.i_b);
+            x.bo = vec(L.o_b); x.bdown = vec(L.o2_b);
+            x.l1w = vec(L.ln_att_w); x.l1b = vec(L.ln_att_b); x.l2w = vec(L.ln_out_w); x.l2b = vec(L.ln_out_b);
+            continue;
+        }
         x.qkv = linear({&L.q_w, &L.k_w, &L.v_w});
         x.o = linear({&L.o_w});
         x.up = linear({&L.i_w});
@@ -348,6 +374,14 @@ void Device::upload(const HostModel &m)
     for (int l = 0; l < hp_.n_layer; ++l) {
         const LIdx &x = li[(size_t)l];
         DevLayer &D = layers_[(size_t)l];
+        if (f32_) {
+            D.w32_qkv = (const float *)P(x.w32q); D.w32_o = (const float *)P(x.w32o);
+            D.w32_up = (const float *)P(x.w32u); D.w32_down = (const float *)P(x.w32d);
+            D.b_qkv = (const float *)P(x.bq); D.b_up = (const float *)P(x.bu);
+            D.b_o = (float *)P(x.bo); D.b_down = (float *)P(x.bdown);
+            D.ln1_w = (float *)P(x.l1w); D.ln1_b = (float *)P(x.l1b); D.ln2_w = (float *)P(x.l2w); D.ln2_b = (float *)P(x.l2b);
+            continue;
+        }
         D.qkv = mk_lin(x.qkv); D.o = mk_lin(x.o); D.up = mk_lin(x.up); D.down = mk_lin(x.down);
         D.b_o = (float *)P(x.bo); D.b_down = (float *)P(x.bdown);
         D.c1_qkv = (float *)P(x.c1q); D.c2_qkv = (float *)P(x.c2q); D.c1_up = (float *)P(x.c1u); D.c2_up = (float *)P(x.c2u);
@@ -373,8 +407,12 @@ bool Device::reserve(int64_t tokens, int64_t seqs, int max_len)
     const int64_t d = hp_.n_embd, f = hp_.n_intermediate;
     size_t off = 0;
     auto take = [&](size_t bytes) { size_t o = off; off += align_up(bytes, 256); return o; };
-    const size_t o_st = take(rows * 8), o_z = take(rows * d * 2), o_part = take(rows * (d / 32) * 8);
-    const size_t o_qkv = take(rows * 3 * d * 2), o_att = take(rows * d * 2), o_ffn = take(rows * f * 2);
+    // f16 chain: Z, QKV, ATT, FFN f16 + statistics; f32 chain: X, Z, QKV, ATT, FFN f32
+    const int64_t r16 = f32_ ? 0 : rows, r32 = f32_ ? rows : 0;
+    const size_t o_st = take(r16 * 8), o_z = take(r16 * d * 2), o_part = take(r16 * (d / 32) * 8);
+    const size_t o_qkv = take(r16 * 3 * d * 2), o_att = take(r16 * d * 2), o_ffn = take(r16 * f * 2);
+    const size_t o_x32 = take(r32 * d * 4), o_z32 = take(r32 * d * 4), o_qkv32 = take(r32 * 3 * d * 4);
+    const size_t o_att32 = take(r32 * d * 4), o_ffn32 = take(r32 * f * 4);
     const size_t o_ids = take(rows * 4), o_cu = take((ns + 1) * 4), o_out = take(ns * d * 4);
     const size_t o_pool = take((size_t)np * d * 4);
     drop_graphs();   // captured graphs hold the old workspace pointers
@@ -393,6 +431,8 @@ bool Device::reserve(int64_t tokens, int64_t seqs, int max_len)
     qkv_ = (uint16_t *)(ws_ + o_qkv); att_ = (uint16_t *)(ws_ + o_att); ffn_ = (uint16_t *)(ws_ + o_ffn);
     d_ids_ = (int32_t *)(ws_ + o_ids); d_cu_ = (int32_t *)(ws_ + o_cu); d_out_ = (float *)(ws_ + o_out);
     pool_part_ = (float *)(ws_ + o_pool);
+    x32_ = (float *)(ws_ + o_x32); z32_ = (float *)(ws_ + o_z32); qkv32_ = (float *)(ws_ + o_qkv32);
+    att32_ = (float *)(ws_ + o_att32); ffn32_ = (float *)(ws_ + o_ffn32);
     HIP_OK(hipHostMalloc((void **)&h_ids_, nt * 4, hipHostMallocDefault));
     HIP_OK(hipHostMalloc((void **)&h_cu_, (ns + 1) * 4, hipHostMallocDefault));
     HIP_OK(hipHostMalloc((void **)&h_out_, ns * d * 4, hipHostMallocDefault));
@@ -520,6 +560,7 @@ int Device::forward_ordered(const int32_t *d_ids, const int32_t *d_cu, int n_seq
 int Device::launch_all(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, int max_len, int T, float *d_out,
                        hipStream_t s, bool check)
 {
+    if (f32_) return launch_all_f32(d_ids, d_cu, n_seqs, max_len, T, d_out, s);
     const int d = hp_.n_embd, f = hp_.n_intermediate;
     const int M = gemm_rows(T);   // GEMM rows: T padded to whole tiles
     const double t = (double)T;
@@ -603,6 +644,54 @@ int Device::launch_all(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, in
     end(K_POOL_L2, s, ev, t * d * 2.0 + t * 8.0 + (double)n_seqs * d * 4.0);
     chk("pool_l2", -1, d_out, (size_t)n_seqs * d, 0);
     if (cnt) (void)hipFree(cnt);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        std::fprintf(stderr, "libbert: kernel launch failed: %s\n", hipGetErrorString(e));
+        return -1;
+    }
+    return 0;
+}
+
+// The f32 chain (ftype 0 files, f32.hip): bert.cpp:963-1095 with every tensor in
+// f32, the reference's own op order (QKV + bias, attention, (bias + O) + x, LN,
+// GELU(bias + FFN-up), z + (bias + FFN-down), LN; mean pool, divide by the norm).
+int Device::launch_all_f32(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, int max_len, int T, float *d_out,
+                           hipStream_t s)
+{
+    const int d = hp_.n_embd, f = hp_.n_intermediate;
+    const int M = gemm_rows(T);
+    const double t = (double)T;
+    hipEvent_t ev;
+    begin(K_EMBED_LN, s, ev);
+    launch_f32_embed_ln(word_, type_, pos_, ln_e_w_, ln_e_b_, d_ids, d_cu, n_seqs, max_len, d, x32_, s);
+    end(K_EMBED_LN, s, ev, t * (4.0 + 3.0 * d * 4.0 + 4.0 * d));
+    for (int l = 0; l < hp_.n_layer; ++l) {
+        const DevLayer &L = layers_[(size_t)l];
+        begin(K_GEMM_QKV, s, ev);
+        if (launch_f32_gemm(x32_, M, L.w32_qkv, 3 * d, d, L.b_qkv, 0, nullptr, qkv32_, s)) return -1;
+        end(K_GEMM_QKV, s, ev, 2.0 * t * 3.0 * d * d);
+        begin(K_ATTENTION, s, ev);
+        if (launch_f32_attention(qkv32_, d_cu, n_seqs, max_len, hp_.n_head, d, att32_, s)) return -1;
+        end(K_ATTENTION, s, ev, att_flop_);
+        begin(K_GEMM_O, s, ev);
+        if (launch_f32_gemm(att32_, M, L.w32_o, d, d, L.b_o, 2, x32_, z32_, s)) return -1;
+        end(K_GEMM_O, s, ev, 2.0 * t * d * d);
+        begin(K_LN_STATS, s, ev);
+        launch_f32_ln(z32_, M, d, L.ln1_w, L.ln1_b, s);
+        end(K_LN_STATS, s, ev, (double)M * d * 8.0);
+        begin(K_GEMM_FFN_UP, s, ev);
+        if (launch_f32_gemm(z32_, M, L.w32_up, f, d, L.b_up, 1, nullptr, ffn32_, s)) return -1;
+        end(K_GEMM_FFN_UP, s, ev, 2.0 * t * d * f);
+        begin(K_GEMM_FFN_DOWN, s, ev);
+        if (launch_f32_gemm(ffn32_, M, L.w32_down, d, f, L.b_down, 2, z32_, x32_, s)) return -1;
+        end(K_GEMM_FFN_DOWN, s, ev, 2.0 * t * d * f);
+        begin(K_LN_STATS, s, ev);
+        launch_f32_ln(x32_, M, d, L.ln2_w, L.ln2_b, s);
+        end(K_LN_STATS, s, ev, (double)M * d * 8.0);
+    }
+    begin(K_POOL_L2, s, ev);
+    launch_f32_pool(x32_, d_cu, n_seqs, d, d_out, s);
+    end(K_POOL_L2, s, ev, t * d * 4.0 + (double)n_seqs * d * 4.0);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         std::fprintf(stderr, "libbert: kernel launch failed: %s\n", hipGetErrorString(e));
@@ -763,6 +852,30 @@ extern "C" int32_t bertx_test_gemm_ln(int32_t fmt, int32_t N, int32_t K, const v
     HIP_RC(hipDeviceSynchronize());
     HIP_RC(hipMemcpy(out, dout, (size_t)M * N * 2, hipMemcpyDeviceToHost));
     if (dst && st_out) HIP_RC(hipMemcpy(st_out, dst, (size_t)M * 8, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+// f32 chain GEMM (f32.hip) on host buffers: w f32 [N][K], x f32 [M][K], res/out f32 [M][N]
+extern "C" int32_t bertx_test_gemm_f32(int32_t N, int32_t K, const float *w, const float *bias, int32_t M,
+                                       const float *x, int32_t epi, const float *res, float *out)
+{
+    using namespace emb;
+    if (N <= 0 || K % 32 || K <= 0 || M <= 0 || epi < 0 || epi > 2 || (epi == 2 && !res) || hip_device_count() == 0)
+        return -1;
+    const int Mp = (int)align_up((size_t)M, 64);
+    DeviceGuard guard(0);
+    HIP_RC(guard.status());
+    HookBufs B;
+    const float *dw = (const float *)B.up(w, (size_t)N * K * 4, 0);
+    const float *db = (const float *)B.up(bias, (size_t)N * 4, 0);
+    const float *dx = (const float *)B.up(x, (size_t)M * K * 4, (size_t)Mp * K * 4);
+    const float *dr = epi == 2 ? (const float *)B.up(res, (size_t)M * N * 4, (size_t)Mp * N * 4) : nullptr;
+    float *dout = (float *)B.up(nullptr, 0, (size_t)Mp * N * 4);
+    if (B.bad) return -1;
+    if (launch_f32_gemm(dx, Mp, dw, N, K, db, epi, dr, dout, nullptr) != 0) return -1;
+    HIP_RC(hipGetLastError());
+    HIP_RC(hipDeviceSynchronize());
+    HIP_RC(hipMemcpy(out, dout, (size_t)M * N * 4, hipMemcpyDeviceToHost));
     return 0;
 }
 

@@ -35,6 +35,10 @@ struct DevLayer {
     // output LN or the embedding LN; FFN-up: this layer's attention-output LN)
     float *c1_qkv = nullptr, *c2_qkv = nullptr, *c1_up = nullptr, *c2_up = nullptr;
     float *ln1_w = nullptr, *ln1_b = nullptr, *ln2_w = nullptr, *ln2_b = nullptr;
+    // f32 files (the f32 chain, f32.hip): weights as the file rows [N][K] f32, QKV
+    // fused [3d][d] with its bias [3d]
+    const float *w32_qkv = nullptr, *w32_o = nullptr, *w32_up = nullptr, *w32_down = nullptr;
+    const float *b_qkv = nullptr, *b_up = nullptr;
 };
 
 // Sets the calling thread's current HIP device for a scope and restores the
@@ -122,6 +126,8 @@ private:
     void mark_done(hipStream_t s);          // records the completion event of a forward on s
     int launch_all(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, int max_len, int T, float *d_out,
                    hipStream_t s, bool check);
+    int launch_all_f32(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, int max_len, int T, float *d_out,
+                       hipStream_t s);
     void drop_graphs();
     void upload(const HostModel &m);
     void *arena_alloc(size_t bytes);
@@ -142,6 +148,7 @@ private:
     float *ln_e_w_ = nullptr, *ln_e_b_ = nullptr;
     std::vector<DevLayer> layers_;
     int wfmt_ = FMT_F16;
+    bool f32_ = false;              // ftype 0 file: the f32 chain (f32.hip)
 
     // workspace
     int64_t cap_tokens_ = 0, cap_seqs_ = 0, cap_pool_ = 0;   // cap_pool_: pool partial rows (seqs x chunks)
@@ -154,6 +161,7 @@ private:
     float2 *part_ = nullptr;        // [d/32][rows] group partials of the residual GEMMs
     int64_t rows_ = 0;              // workspace rows (part_ stride)
     uint16_t *qkv_ = nullptr, *att_ = nullptr, *ffn_ = nullptr;
+    float *x32_ = nullptr, *z32_ = nullptr, *qkv32_ = nullptr, *att32_ = nullptr, *ffn32_ = nullptr;   // f32 chain
     int32_t *d_ids_ = nullptr, *d_cu_ = nullptr;
     float *d_out_ = nullptr;
     float *pool_part_ = nullptr;

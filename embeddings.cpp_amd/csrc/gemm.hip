@@ -137,10 +137,78 @@ constexpr int zepi_lds()
     return 1024 * (zkib(zepi_arrays<EPI, LNF>() * BN * 4) + (LNF ? zkib(BM * 8) : 0));
 }
 
+// vmcnt accounting of the K loop, derived instead of hand-counted.  Each wave
+// issues per K-step one weight group W(k) of LQ loads (into a register set of
+// the WR-deep ring, WR - 1 steps ahead) and one X group X(k) of XG LDS-DMA loads
+// (into the NS-stage LDS ring, NS - 1 steps ahead); vmcnt retires in issue
+// order, so a wait that must see group G complete may leave at most the loads
+// issued after G's last load in flight.  z_waits replays the issue order the
+// kernel uses (its prologue, then per step the two groups in kernel order; the
+// tail clamps k but still issues every load, so counts are the same on every
+// path) and returns, for each wait, the minimum over steps of that count:
+//   prologue: W(0) and X(0) complete (then the barrier publishes X(0));
+//   front of step ks: W(ks) complete (the registers its MFMAs dequantize);
+//   back of step ks: X(ks + 1) and W(ks + 1) complete (then the barrier
+//   publishes X(ks + 1) to every wave before step ks + 1 reads it).
+// The minimum matters: with a deeper ring the steps right after the prologue
+// have fewer loads in flight behind W(ks) than the steady state (the prologue
+// issues its groups in another order), so a constant read off the steady
+// state leaves those W(ks) unretired ("the 4-set ring race").
+struct ZWaits { int prologue, front, back; };
+
+template <int NS, int WR, int LQ, int XG>
+constexpr ZWaits z_waits()
+{
+    constexpr int S = 16;                        // steps replayed (periodic long before)
+    int kind[3 * S + 16] = {}, kk[3 * S + 16] = {}, ops[3 * S + 16] = {};
+    int n = 0;
+    auto add = [&](int kd, int k) { kind[n] = kd; kk[n] = k; ops[n] = kd == 0 ? LQ : XG; ++n; };
+    auto after = [&](int kd, int k) {            // loads issued after group (kd, k)'s last load
+        int last = -1;
+        for (int i = 0; i < n; ++i)
+            if (kind[i] == kd && kk[i] == k) last = i;
+        int c = 0;
+        for (int i = last + 1; i < n; ++i) c += ops[i];
+        return last < 0 ? -1 : c;
+    };
+    auto mn = [](int a, int b) { return a < b ? a : b; };
+    // prologue, in the kernel's order (gemmz_body)
+    if (NS == 2) { add(0, 0); add(1, 0); add(0, 1); }
+    else if (NS == 3) { add(0, 0); add(1, 0); add(0, 1); add(1, 1); }
+    else { add(0, 0); add(1, 0); add(1, 1); add(0, 1); add(1, 2); }
+    for (int j = 2; j < WR - 1; ++j) add(0, j);
+    ZWaits w{mn(after(0, 0), after(1, 0)), 1 << 20, 1 << 20};
+    for (int ks = 0; ks < S; ++ks) {
+        if (NS == 2) { add(1, ks + 1); add(0, ks + WR - 1); }
+        else { add(0, ks + WR - 1); add(1, ks + NS - 1); }
+        w.front = mn(w.front, after(0, ks));
+        w.back = mn(w.back, mn(after(1, ks + 1), after(0, ks + 1)));
+    }
+    return w;
+}
+
+// The production ring (WR = 3) against the counts the kernel carried before the
+// derivation (2P + XG in front, P + XG behind at NS 4): equal; at NS 2
+// the old front count 2 LQ + XG also retired X(ks), already retired by the
+// previous step's back wait, so the derived 2 (LQ + XG) waits for the same loads.
+static_assert(z_waits<4, 3, 2, 4>().front == 2 * 6 + 4 && z_waits<4, 3, 2, 4>().back == 6 + 4 &&
+                  z_waits<4, 3, 2, 4>().prologue == 6 + 4,
+              "derived waits, 128x128 / 64x64 q4_0");
+static_assert(z_waits<4, 3, 4, 4>().front == 2 * 8 + 4 && z_waits<4, 3, 4, 4>().back == 8 + 4,
+              "derived waits, 64x64 f16");
+static_assert(z_waits<2, 3, 2, 8>().front == 2 * (2 + 8) && z_waits<2, 3, 2, 8>().back == 2 &&
+                  z_waits<2, 3, 2, 8>().prologue == 2,
+              "derived waits, 256x128 q4_0");
+// the 4-set ring: the steady state has 3P + XG behind W(ks) (q4_0: 22) but the
+// two steps after the prologue only 3P (18)
+static_assert(z_waits<4, 4, 2, 4>().front == 3 * 6 && z_waits<4, 4, 2, 4>().back == 2 * 6 &&
+                  z_waits<4, 4, 2, 4>().prologue == 2 * 6,
+              "derived waits, 4-set ring");
+
 // The tile body: workgroup b of a grid of nTiles tiles (nN column tiles),
 // staging X in `smem` (NS * BM * 128 B of LDS) and the epilogue operands
 // behind it (zepi_lds).
-template <int FMT, int EPI, bool LNF, int NW, int BM, int NS, int FA>
+template <int FMT, int EPI, bool LNF, int NW, int BM, int NS, int FA, int WR>
 __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b, DevWeight W,
                                            const h16 *__restrict__ X, const float *__restrict__ bias,
                                            const void *__restrict__ res, void *__restrict__ out, int nN, int nTiles,
@@ -155,6 +223,11 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     constexpr int QB = ZRegs<FMT>::QB;
     constexpr int P = LQ + XG;                  // vector-memory ops issued per K-step per wave
     static_assert(NS >= 2 && NS <= 4 && XG >= 2 && XG % 2 == 0, "X ring");
+    static_assert(WR == 3 || WR == 4, "weight register ring: 3 or 4 sets");
+    constexpr ZWaits ZW = z_waits<NS, WR, LQ, XG>();
+    static_assert(ZW.prologue >= 0 && ZW.front >= 0 && ZW.back >= 0 && ZW.front < 64 && P <= 63,
+                  "vmcnt range (6 bits)");
+    (void)P;
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     ZSTAMP(0, __builtin_amdgcn_s_memtime());
     // XCD-aware bijective remap: consecutive tiles (same token panel) land on one
@@ -236,27 +309,29 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[a][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    ZSet<FMT, FA> w0, w1, w2;
+    ZSet<FMT, FA> w0, w1, w2, w3;
     const int k1 = min(1, KS - 1);
     wload(w0, 0);
     issue_x(0, 0);
     if constexpr (NS == 2) {
         wload(w1, k1);
-        wait_vmcnt<LQ>();
     } else if constexpr (NS == 3) {
         asm volatile("" ::: "memory");
         wload(w1, k1);
         asm volatile("" ::: "memory");
         issue_x(k1, 1);
-        wait_vmcnt<P>();
     } else {
         issue_x(k1, 1);
         asm volatile("" ::: "memory");
         wload(w1, k1);
         asm volatile("" ::: "memory");
         issue_x(min(2, KS - 1), 2);
-        wait_vmcnt<P + XG>();
     }
+    if constexpr (WR == 4) {
+        asm volatile("" ::: "memory");
+        wload(w2, min(2, KS - 1));
+    }
+    wait_vmcnt<ZW.prologue>();
     lds_barrier();
     ZSTAMP(1, __builtin_amdgcn_s_memtime());
 
@@ -269,26 +344,27 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     unsigned long long zw_front = 0, zw_back = 0;
 #endif
     // One K-step with CUR's weights: issue X(ks + NS - 1) into the stage freed by
-    // the previous step and W(ks + 2) into the third register set, then an
-    // explicit vmcnt equal to what is provably still in flight (a run-time no-op
-    // that stops hipcc's waitcnt pass from draining the ring with vmcnt(0)); the
-    // K loop runs whole, unguarded triples so the count holds on every path.
-    auto kstep = [&](ZSet<FMT, FA> &cur, ZSet<FMT, FA> &nxt2, int ks) {
-        const int kx = min(ks + NS - 1, KS - 1), k2 = min(ks + 2, KS - 1);
+    // the previous step and W(ks + WR - 1) into the ring's free register set,
+    // then the derived vmcnt (z_waits: what is provably still in flight; a
+    // run-time no-op that stops hipcc's waitcnt pass from draining the ring with
+    // vmcnt(0)); the K loop runs whole, unguarded WR-tuples so the count holds
+    // on every path.
+    auto kstep = [&](ZSet<FMT, FA> &cur, ZSet<FMT, FA> &nxt, int ks) {
+        const int kx = min(ks + NS - 1, KS - 1), kw = min(ks + WR - 1, KS - 1);
         const int sx = st == 0 ? NS - 1 : st - 1;
         if constexpr (NS == 2) {
             issue_x(kx, sx);
             asm volatile("" ::: "memory");
-            wload(nxt2, k2);
-            wait_vmcnt<2 * LQ + XG>();
+            wload(nxt, kw);
+            wait_vmcnt<ZW.front>();
         } else {
-            wload(nxt2, k2);
+            wload(nxt, kw);
             asm volatile("" ::: "memory");
             issue_x(kx, sx);
 #ifdef GEMM_STAMPS
             const unsigned long long za = __builtin_amdgcn_s_memtime();
 #endif
-            wait_vmcnt<2 * P + (NS == 4 ? XG : 0)>();
+            wait_vmcnt<ZW.front>();
 #ifdef GEMM_STAMPS
             zw_front += __builtin_amdgcn_s_memtime() - za;
 #endif
@@ -300,9 +376,7 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
 #ifdef GEMM_STAMPS
         const unsigned long long zb = __builtin_amdgcn_s_memtime();
 #endif
-        if constexpr (NS == 2) wait_vmcnt<LQ>();
-        else if constexpr (NS == 3) wait_vmcnt<P>();
-        else wait_vmcnt<P + XG>();
+        wait_vmcnt<ZW.back>();
         lds_barrier();
 #ifdef GEMM_STAMPS
         zw_back += __builtin_amdgcn_s_memtime() - zb;
@@ -310,14 +384,28 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
         st = st == NS - 1 ? 0 : st + 1;
     };
     int ks = 0;
-    for (; ks + 3 <= KS; ks += 3) {
-        kstep(w0, w2, ks);
-        kstep(w1, w0, ks + 1);
-        kstep(w2, w1, ks + 2);
-    }
-    if (ks < KS) {
-        kstep(w0, w2, ks);
-        if (ks + 1 < KS) kstep(w1, w0, ks + 1);
+    if constexpr (WR == 3) {
+        for (; ks + 3 <= KS; ks += 3) {
+            kstep(w0, w2, ks);
+            kstep(w1, w0, ks + 1);
+            kstep(w2, w1, ks + 2);
+        }
+        if (ks < KS) {
+            kstep(w0, w2, ks);
+            if (ks + 1 < KS) kstep(w1, w0, ks + 1);
+        }
+    } else {
+        for (; ks + 4 <= KS; ks += 4) {
+            kstep(w0, w3, ks);
+            kstep(w1, w0, ks + 1);
+            kstep(w2, w1, ks + 2);
+            kstep(w3, w2, ks + 3);
+        }
+        if (ks < KS) {
+            kstep(w0, w3, ks);
+            if (ks + 1 < KS) kstep(w1, w0, ks + 1);
+            if (ks + 2 < KS) kstep(w2, w1, ks + 2);
+        }
     }
     wait_vmcnt<0>();
     ZSTAMP(2, __builtin_amdgcn_s_memtime());
@@ -466,7 +554,7 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     }
 }
 
-template <int FMT, int EPI, bool LNF, int NW, int BM, int NS, int FA>
+template <int FMT, int EPI, bool LNF, int NW, int BM, int NS, int FA, int WR>
 __global__ __launch_bounds__(64 * NW, 2) void gemmz_kernel(DevWeight W, const h16 *__restrict__ X,
                                                                const float *__restrict__ bias,
                                                                const void *__restrict__ res, void *__restrict__ out,
@@ -478,13 +566,13 @@ __global__ __launch_bounds__(64 * NW, 2) void gemmz_kernel(DevWeight W, const h1
     // so no wave leaves the body early and the barrier between tiles is reached
     // by all)
     for (int b = blockIdx.x; b < nTiles; b += gridDim.x) {
-        gemmz_body<FMT, EPI, LNF, NW, BM, NS, FA>(smem, b, W, X, bias, res, out, nN, nTiles, ln);
+        gemmz_body<FMT, EPI, LNF, NW, BM, NS, FA, WR>(smem, b, W, X, bias, res, out, nN, nTiles, ln);
         ZSTAMP(3, __builtin_amdgcn_s_memtime());
         if (b + (int)gridDim.x < nTiles) lds_barrier();   // LDS (X ring, epilogue operands) reused
     }
 }
 
-template <int FMT, int NW, int BM, int NS, int FA = 1>
+template <int FMT, int NW, int BM, int NS, int FA = 1, int WR = 3>
 void dispatch_z(const DevWeight &W, const h16 *x, int M, const float *bias, int epi, const void *res, void *out,
                 hipStream_t s, const LnFold &ln, bool lnf)
 {
@@ -503,14 +591,14 @@ void dispatch_z(const DevWeight &W, const h16 *x, int M, const float *bias, int 
     if (persist > 0 && W.N % BN == 0) grid = std::min(nTiles, persist * cus);
     auto go = [&](auto kern) { kern<<<grid, 64 * NW, 0, s>>>(W, x, bias, res, out, nN, nTiles, ln); };
     if (epi == EPI_BIAS_F16) {
-        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_F16, true, NW, BM, NS, FA>);
-        else go(gemmz_kernel<FMT, EPI_BIAS_F16, false, NW, BM, NS, FA>);
+        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_F16, true, NW, BM, NS, FA, WR>);
+        else go(gemmz_kernel<FMT, EPI_BIAS_F16, false, NW, BM, NS, FA, WR>);
     } else if (epi == EPI_BIAS_GELU_F16) {
-        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_GELU_F16, true, NW, BM, NS, FA>);
-        else go(gemmz_kernel<FMT, EPI_BIAS_GELU_F16, false, NW, BM, NS, FA>);
+        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_GELU_F16, true, NW, BM, NS, FA, WR>);
+        else go(gemmz_kernel<FMT, EPI_BIAS_GELU_F16, false, NW, BM, NS, FA, WR>);
     } else {
-        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_RES, true, NW, BM, NS, FA>);
-        else go(gemmz_kernel<FMT, EPI_BIAS_RES, false, NW, BM, NS, FA>);
+        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_RES, true, NW, BM, NS, FA, WR>);
+        else go(gemmz_kernel<FMT, EPI_BIAS_RES, false, NW, BM, NS, FA, WR>);
     }
 }
 
@@ -528,6 +616,7 @@ void launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, 
     if (cfg == 2 && M % 256 == 0) dispatch_z<FMT, 4, 256, 2>(W, x, M, bias, epi, res, out, s, ln, lnf);
     else if (cfg == 5 && M % 128 == 0) dispatch_z<FMT, 4, 128, 4, 2>(W, x, M, bias, epi, res, out, s, ln, lnf);
     else if (cfg != 4 && M % 128 == 0) dispatch_z<FMT, 4, 128, 4>(W, x, M, bias, epi, res, out, s, ln, lnf);
+    else if (cfg == 6 && M % 64 == 0) dispatch_z<FMT, 2, 64, 4, 1, 4>(W, x, M, bias, epi, res, out, s, ln, lnf);
     else dispatch_z<FMT, 2, 64, 4>(W, x, M, bias, epi, res, out, s, ln, lnf);
 }
 

@@ -92,7 +92,7 @@ struct LnFold {
 int launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi,
                 const void *res, void *out, hipStream_t s, const LnFold &ln = LnFold());
 // Tests/benches: tile config (0 = heuristic, 2 = 4 waves 256x128, 3 = 4 waves 128x128,
-// 4 = 2 waves 64x64).
+// 4 = 2 waves 64x64, 5 = 4 waves 128x256, 6 = 64x64 with the 4-set weight ring).
 // Per calling thread, so a test hook never changes a forward running on another thread.
 extern thread_local int g_gemm_cfg;
 
@@ -124,6 +124,24 @@ void launch_attention(const uint16_t *qkv, const int32_t *cu, int32_t n_seqs, in
 int32_t pool_chunks(int32_t max_len);
 void launch_pool_l2(const uint16_t *z, const float2 *stats, const float *ln_w, const float *ln_b, const int32_t *cu,
                     int32_t n_seqs, int32_t max_len, int32_t d, float *partial, float *out, hipStream_t s);
+
+// ---- the f32 chain (ftype 0 files, f32.hip): every activation f32 [rows][width] ----
+// x = LN(pos + (type + word)) with gamma/beta (bert.cpp:963-984).
+void launch_f32_embed_ln(const DevTable &word, const DevTable &type, const DevTable &pos, const float *ln_w,
+                         const float *ln_b, const int32_t *ids, const int32_t *cu, int32_t n_seqs, int32_t max_len,
+                         int32_t d, float *x, hipStream_t s);
+// In-place LayerNorm of rows [0, rows) (ggml_norm, f64 sums, eps 1e-5).
+void launch_f32_ln(float *x, int32_t rows, int32_t d, const float *g, const float *b, hipStream_t s);
+// Y[M][N] = epi(X[M][K] W[N][K]^T): 0 bias + acc, 1 era GELU(bias + acc), 2 (bias + acc)
+// + res.  M % 64 == 0, K % 32 == 0; returns -1 otherwise.
+int launch_f32_gemm(const float *X, int32_t M, const float *W, int32_t N, int32_t K, const float *bias, int32_t epi,
+                    const float *res, float *Y, hipStream_t s);
+// Per (sentence, head) softmax(Q K^T / sqrt(dh)) V with the era's fp16-table exp,
+// qkv f32 [T][3d] -> out f32 [T][d]; dh 32 or 64, max_len <= 2048, else -1.
+int launch_f32_attention(const float *qkv, const int32_t *cu, int32_t n_seqs, int32_t max_len, int32_t n_head,
+                         int32_t d, float *out, hipStream_t s);
+// out[b] = mean_{i<len} x[start + i] / ||.|| (bert.cpp:1087-1095).
+void launch_f32_pool(const float *x, const int32_t *cu, int32_t n_seqs, int32_t d, float *out, hipStream_t s);
 
 // Diagnostics: *cnt += number of non-finite values in p[0..n) (f32, or f16 if f16).
 void launch_count_nonfinite(const void *p, size_t n, int f16, unsigned *cnt, hipStream_t s);

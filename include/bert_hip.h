@@ -82,7 +82,8 @@ BERT_API int32_t bertx_convert_hf(const char *dir_model, const char *fname_out, 
  * 1 = +bias, era GELU -> f16, 2 = +bias +res -> f16 (res f16 [M][N], the
  * residual-stream form; sum in f32, computed in place over res).  cfg: GEMM tile
  * config (0 = the production heuristic, 2 = 4 waves 256x128, 3 = 4 waves 128x128,
- * 4 = 2 waves 64x64).
+ * 4 = 2 waves 64x64, 5 = 4 waves 128x256, 6 = 2 waves 64x64 with a 4-set weight
+ * register ring).
  * Reference interface these kernels replace: ggml_mul_mat + ggml_add (+ ggml_gelu)
  * at bert.cpp:994-1016, 1040-1045, 1059-1072.
  */
@@ -107,6 +108,16 @@ BERT_API int32_t bertx_test_gemm_ln(int32_t fmt, int32_t N, int32_t K, const voi
                                     const float *in_b, int32_t epi, const uint16_t *res, const float *res_stats,
                                     const float *res_g, const float *res_b, const float *g_next, uint16_t *out,
                                     float *st_out, int32_t cfg);
+
+/*
+ * The f32 chain's GEMM (ftype 0 files: f32 activations x f32 weights on
+ * v_mfma_f32_16x16x4_f32, reference ggml_mul_mat f32 x f32, bert.cpp:995):
+ * w f32 [N][K] (file rows), x f32 [M][K], out f32 [M][N] = epi(x w^T):
+ * epi 0 = bias + acc, 1 = era GELU(bias + acc) (fp16-table semantics), 2 =
+ * (bias + acc) + res (res f32 [M][N]).  K % 32 == 0.  Returns 0 or -1.
+ */
+BERT_API int32_t bertx_test_gemm_f32(int32_t N, int32_t K, const float *w, const float *bias, int32_t M,
+                                     const float *x, int32_t epi, const float *res, float *out);
 
 /*
  * GEMM micro-benchmark on random operands (device 0): average device time of

@@ -45,20 +45,22 @@ def test_forward_matches_oracle(quant_models, tiny, fmt):
     assert np.allclose(np.linalg.norm(got, axis=1), 1.0, atol=1e-5)
 
 
+F32_COS_TOL = 1e-6   # f32 files: f32 x f32 like the reference (bert.cpp:499-503)
+
+
 @pytest.mark.parametrize("tiny", ["tiny32", "tiny64"])
-def test_f32_weights_as_tight_as_f16(quant_models, tiny):
-    """f32 files run with f32-accurate weights (f16 hi/lo pairs, engine.cpp repack_linear_f32),
-    not rounded to f16: the f32 model's distance to the oracle's f32 forward (bert.cpp:499-503,
-    f32 x f32) is at most the f16 model's distance to the oracle's f16 forward."""
-    dev = {}
-    for fmt in ("f32", "f16"):
-        path = quant_models[(tiny, fmt)]
-        m = bertpy.BertModel(path)
-        o = oracle_lib.Oracle(path)
-        ids = ragged_ids(o.n_vocab, [2, 3, 17, 64, 100, m.n_max_tokens - 1, m.n_max_tokens, 33])
-        dev[fmt] = float(1.0 - cosines(m.forward_batch(ids), o.forward_batch(ids)).min())
-    print("1 - min cosine vs oracle:", dev)
-    assert dev["f32"] <= max(dev["f16"], 2e-7), dev
+def test_f32_file_at_f32_precision(quant_models, tiny):
+    """f32 files run the f32 chain (f32.hip: f32 activations x f32 weights, the era's
+    fp16-table softmax exp and GELU as the reference applies them): 1 - cos <= 1e-6
+    against the oracle's f32 forward on ragged lengths up to n_max_tokens, an
+    absolute bound three orders tighter than the f16 paths'."""
+    path = quant_models[(tiny, "f32")]
+    m = bertpy.BertModel(path)
+    o = oracle_lib.Oracle(path)
+    ids = ragged_ids(o.n_vocab, [2, 3, 17, 64, 100, m.n_max_tokens - 1, m.n_max_tokens, 33])
+    c = cosines(m.forward_batch(ids), o.forward_batch(ids))
+    print(tiny, "f32 chain: 1 - min cos vs oracle", float(1.0 - c.min()))
+    assert np.all(c >= 1 - F32_COS_TOL), 1.0 - c
 
 
 @pytest.mark.parametrize("tiny", ["tiny32", "tiny64"])

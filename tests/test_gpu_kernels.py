@@ -97,6 +97,63 @@ def test_gemm_matches_numpy(lib, fmt, epi, shape):
         assert np.abs(got - exact).max() <= 5e-3 * np.abs(exact).max()
 
 
+@pytest.mark.parametrize("epi", [0, 1, 2])
+@pytest.mark.parametrize("N,K,M", [(1152, 384, 96), (384, 1536, 64), (96, 64, 130), (40, 32, 7)])
+def test_f32_gemm_matches_numpy(lib, epi, N, K, M):
+    """The f32 chain's GEMM (f32.hip, ftype 0 files: f32 x f32 as bert.cpp:995 multiplies
+    them) against numpy f64: an f32 FMA chain over K, so the error is a few f32 ulps of
+    sum |x w| -- far below any f16 path."""
+    rng = np.random.default_rng(N + K + M + epi)
+    W = rng.standard_normal((N, K)).astype(np.float32) * 0.05
+    b = rng.standard_normal(N).astype(np.float32) * 0.1
+    X = rng.standard_normal((M, K)).astype(np.float32)
+    R = rng.standard_normal((M, N)).astype(np.float32)
+    out = np.zeros((M, N), np.float32)
+    rc = lib.bertx_test_gemm_f32(N, K, W.ctypes.data, b.ctypes.data, M, X.ctypes.data, epi,
+                                 R.ctypes.data if epi == 2 else None, out.ctypes.data)
+    assert rc == 0
+    acc = X.astype(np.float64) @ W.astype(np.float64).T + b
+    mag = np.abs(X).astype(np.float64) @ np.abs(W).astype(np.float64).T + np.abs(b)
+    if epi == 1:
+        # the era table: gelu(f16(x)) rounded to f16 -- compare on the same f16 input
+        x16 = acc.astype(np.float16).astype(np.float64)
+        ref = (0.5 * x16 * (1 + np.tanh(0.7978845608028654 * x16 * (1 + 0.044715 * x16 * x16)))).astype(np.float16)
+        got16 = out.astype(np.float16)
+        # inputs within 1e-6 of an f16 rounding boundary may land on the neighbour
+        assert np.mean(got16 != ref) < 1e-3
+        assert np.abs(out - ref.astype(np.float64)).max() <= 1e-2 * np.abs(ref).max()
+    else:
+        ref = acc + (R if epi == 2 else 0.0)
+        assert np.all(np.abs(out - ref) <= 4e-7 * (mag + np.abs(R if epi == 2 else 0.0)) + 1e-30)
+
+
+@pytest.mark.parametrize("fmt", sorted(FMTS))
+@pytest.mark.parametrize("cfg", [2, 3, 4, 5, 6])
+def test_gemm_every_k_remainder(lib, cfg, fmt):
+    """Every K-loop length from 1 to 7 K-steps (K = 64 .. 448), every epilogue, for each
+    tile config -- 2: 256x128 (X ring NS 2), 3: 128x128, 4: 64x64, 5: 128x256 (NS 4), 6:
+    64x64 with the 4-set weight ring (WR 4) -- so every remainder of the unrolled K loop
+    (triples for WR 3, quadruples for WR 4) and every prologue clamp runs against numpy.
+    The waits these paths rely on are derived, not hand-counted (gemm.hip z_waits)."""
+    N = {2: 256, 3: 256, 4: 128, 5: 256, 6: 128}[cfg]
+    M = 256
+    for ks in range(1, 8):
+        K = 64 * ks
+        for epi in (0, 1, 2):
+            rng = np.random.default_rng(1000 * cfg + 100 * ks + 10 * epi + fmt)
+            W = rng.standard_normal((N, K)).astype(np.float32) * 0.05
+            W[:, K // 2] *= 20.0
+            bias = rng.standard_normal(N).astype(np.float32) * 0.1
+            X = rng.standard_normal((M, K)).astype(np.float32)
+            res = rng.standard_normal((M, N)).astype(np.float16) if epi == 2 else None
+            got, deq, xh = run_gemm(lib, fmt, W, bias, X, epi, res, cfg)
+            acc = xh.astype(np.float64) @ deq.astype(np.float16).astype(np.float64).T + bias.astype(np.float64)
+            ref = gelu_ref(acc) if epi == 1 else acc + (res.astype(np.float64) if epi == 2 else 0.0)
+            tol = (3e-3 if epi == 1 else 2e-3) * np.abs(ref).max()
+            err = np.abs(got - ref).max()
+            assert err <= tol, (FMTS[fmt], cfg, ks, epi, err, tol)
+
+
 def ln_ref(y):
     """ggml_norm statistics (eps 1e-5, mean then centred variance; bert.cpp:1048-1056) in f64."""
     y = y.astype(np.float64)
