@@ -88,6 +88,8 @@ def load_lib(path=None):
     L.bertx_bench_gemm.argtypes = [c_i32] * 7 + [c_f32p]
     L.bertx_bench_attention.restype = c_i32
     L.bertx_bench_attention.argtypes = [c_i32] * 6 + [c_f32p]
+    L.bertx_tokenize_batch.restype = c_i32
+    L.bertx_tokenize_batch.argtypes = [vp, c_i32, c_i32, ctypes.POINTER(ctypes.c_char_p), c_i32, vp, vp]
     L.bertx_version.restype = ctypes.c_char_p
     L.ggml_time_us.restype = ctypes.c_int64
     if path is None:

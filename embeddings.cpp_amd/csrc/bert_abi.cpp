@@ -7,6 +7,7 @@
 #include "ggml.h"
 
 #include "engine.h"
+#include "task_pool.h"
 #include "tokenizer.h"
 
 #include <algorithm>
@@ -141,6 +142,21 @@ int run_forward(bert_ctx *ctx, const int32_t *const *toks, const int32_t *lens, 
         return rc;
     }
     return 0;
+}
+
+// Tokenize n texts into ids[i * n_max ..] (lens[i] = bert_tokenize's count, which
+// may exceed n_max: bert.cpp:386-387) on up to n_threads threads of the persistent
+// pool; the stage bert_encode_batch runs first (bert.cpp:1402-1406, sequential in
+// the reference).  Blocks of 8 texts per task.
+void tokenize_all(const bert_ctx *ctx, int n_threads, int n, const char *const *texts, int32_t n_max, int32_t *ids,
+                  int32_t *lens)
+{
+    const int64_t n_blocks = ((int64_t)n + 7) / 8;
+    emb::TaskPool::instance().run(n_blocks, n_threads, [&](int64_t blk) {
+        const int e = (int)std::min<int64_t>(n, 8 * blk + 8);
+        for (int i = (int)(8 * blk); i < e; ++i)
+            lens[i] = ctx->vocab.tokenize(texts[i], n_max, ids + (size_t)i * n_max, n_max);
+    });
 }
 
 void print_usage(char **argv, const bert_params &p)
@@ -289,17 +305,7 @@ void bert_encode_batch(struct bert_ctx *ctx, int32_t n_threads, int32_t n_batch_
     const int32_t N = ctx->hp.n_max_tokens;
     std::vector<int32_t> ids((size_t)n_inputs * N);
     std::vector<int32_t> lens((size_t)n_inputs);
-    const int nt = std::max(1, std::min<int>(n_threads > 0 ? n_threads : 1, n_inputs / 8 + 1));
-    auto tok = [&](int t0) {
-        for (int i = t0; i < n_inputs; i += nt)
-            lens[(size_t)i] = ctx->vocab.tokenize(texts[i], N, ids.data() + (size_t)i * N, N);
-    };
-    if (nt == 1) tok(0);
-    else {
-        std::vector<std::thread> th;
-        for (int t = 0; t < nt; ++t) th.emplace_back(tok, t);
-        for (auto &t : th) t.join();
-    }
+    tokenize_all(ctx, n_threads > 0 ? n_threads : 1, n_inputs, texts, N, ids.data(), lens.data());
     // which inputs the reference's chunking refuses (bert.cpp:1408-1443)
     std::vector<char> ok((size_t)n_inputs, 1);
     if (n_batch_size == n_inputs || n_batch_size <= 0) {
@@ -424,6 +430,14 @@ int32_t bertx_quantize_file(const char *fin, const char *fout, int32_t itype)
 int32_t bertx_convert_hf(const char *dir_model, const char *fname_out, int32_t ftype)
 {
     return emb::convert_hf_dir(dir_model, fname_out, ftype);
+}
+
+int32_t bertx_tokenize_batch(struct bert_ctx *ctx, int32_t n_threads, int32_t n_inputs, const char **texts,
+                             int32_t n_max, int32_t *ids, int32_t *n_tokens)
+{
+    if (!ctx || n_inputs < 0 || n_max <= 0 || (n_inputs > 0 && (!texts || !ids || !n_tokens))) return -1;
+    tokenize_all(ctx, n_threads > 0 ? n_threads : 1, n_inputs, texts, n_max, ids, n_tokens);
+    return 0;
 }
 
 const char *bertx_version(void) { return "embeddings.cpp_amd 0.1 (gfx950)"; }

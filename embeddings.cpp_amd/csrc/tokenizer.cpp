@@ -64,6 +64,7 @@ void Vocab::Trie::init(size_t expected)
     keys.assign(cap, 0);
     child.assign(cap, 0);
     term.assign(1, -1);
+    for (int32_t &r : root) r = -1;
     n_nodes = 1;
 }
 
@@ -80,6 +81,7 @@ int32_t Vocab::Trie::step(int32_t node, uint8_t b) const
 
 int32_t Vocab::Trie::add_child(int32_t node, uint8_t b)
 {
+    if (node == 0 && root[b] >= 0) return root[b];
     const uint64_t k = (((uint64_t)node << 8) | b) + 1;
     if ((size_t)n_nodes * 2 >= keys.size()) {     // grow
         std::vector<uint64_t> ok;
@@ -102,6 +104,7 @@ int32_t Vocab::Trie::add_child(int32_t node, uint8_t b)
             keys[i] = k;
             child[i] = n_nodes;
             term.push_back(-1);
+            if (node == 0) root[b] = n_nodes;
             return n_nodes++;
         }
         if (keys[i] == k) return child[i];
@@ -118,9 +121,12 @@ void Vocab::Trie::insert(const char *s, size_t n, int32_t id, bool overwrite)
 
 size_t Vocab::Trie::longest(const char *s, size_t n, int32_t *id) const
 {
-    int32_t node = 0;
+    if (n == 0) return 0;
+    int32_t node = root[(uint8_t)s[0]];
+    if (node < 0) return 0;
     size_t best = 0;
-    for (size_t i = 0; i < n; ++i) {
+    if (term[(size_t)node] >= 0) { best = 1; *id = term[(size_t)node]; }
+    for (size_t i = 1; i < n; ++i) {
         node = step(node, (uint8_t)s[i]);
         if (node < 0) break;
         if (term[(size_t)node] >= 0) { best = i + 1; *id = term[(size_t)node]; }
@@ -167,8 +173,10 @@ int32_t Vocab::tokenize(const char *text, int32_t n_max_tokens, int32_t *out, in
     const uint8_t *in = (const uint8_t *)text;
     const size_t n_in = std::strlen(text);
 
-    // 1) accent strip + A-Z lowercase at character starts (bert.cpp:206-251)
-    std::string a;
+    // 1) accent strip + A-Z lowercase at character starts (bert.cpp:206-251);
+    // per-thread scratch strings keep their capacity across calls
+    thread_local std::string a, b;
+    a.clear();
     a.reserve(n_in);
     for (size_t i = 0; i < n_in;) {
         const size_t len = (size_t)lead_len(in[i]);
@@ -182,7 +190,7 @@ int32_t Vocab::tokenize(const char *text, int32_t n_max_tokens, int32_t *out, in
 
     // 2) isolate ASCII punctuation and 3-byte CJK (bert.cpp:317-339),
     // 3) whitespace split (bert.cpp:341-358) -- fused: collect word spans.
-    std::string b;
+    b.clear();
     b.reserve(a.size() * 2 + 8);
     const uint8_t *pa = (const uint8_t *)a.data();
     for (size_t i = 0; i < a.size();) {

@@ -32,6 +32,7 @@ private:
         std::vector<uint64_t> keys;   // (node << 8 | byte) + 1, 0 = empty
         std::vector<int32_t> child;
         std::vector<int32_t> term;    // node -> token id or -1
+        int32_t root[256];            // the root's children, dense (every word's first byte)
         int32_t n_nodes = 1;
         void init(size_t expected);
         int32_t step(int32_t node, uint8_t b) const;

@@ -148,6 +148,17 @@ BERT_API int32_t bertx_bench_attention(int32_t n_seqs, int32_t len, int32_t n_he
 BERT_API int32_t bertx_test_attention(const uint16_t *qkv, const int32_t *cu, int32_t n_seqs, int32_t n_head,
                                       int32_t d, int32_t variant, uint16_t *out);
 
+/*
+ * The tokenization stage of bert_encode_batch on its own (bert.cpp:1402-1406 runs
+ * it sequentially; here on n_threads threads of the library's persistent pool):
+ * texts[i] -> ids[i * n_max .. + min(n_tokens[i], n_max)), n_tokens[i] =
+ * bert_tokenize's count (which can exceed n_max, bert.cpp:386-387).  The same
+ * function bert_encode_batch calls; for timing and bulk tokenization.  Returns 0
+ * or -1.
+ */
+BERT_API int32_t bertx_tokenize_batch(struct bert_ctx *ctx, int32_t n_threads, int32_t n_inputs, const char **texts,
+                                      int32_t n_max, int32_t *ids, int32_t *n_tokens);
+
 BERT_API const char *bertx_version(void);
 
 #ifdef __cplusplus
