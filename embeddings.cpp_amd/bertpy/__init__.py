@@ -276,6 +276,83 @@ def synthetic_vocab(n_vocab):
     return v[:n_vocab]
 
 
+def bert_like_vocab(n_vocab=30522, seed=0):
+    """A synthetic WordPiece vocab of BERT's size and layout (bert-base-uncased:
+    [PAD], [unused0..98], [UNK]=100, [CLS]=101, [SEP]=102, [MASK]=103, single
+    characters and their '##' forms, then whole words, then '##' word pieces):
+    ASCII punctuation/digits/letters, Latin-1 and Greek letters, 2-byte and 3-byte
+    (CJK) characters, ~21k whole words of 2-14 letters and ~6k '##' pieces of
+    1-6 letters, with a few duplicates (first-wins / last-wins map semantics,
+    bert.cpp:475-494).  Deterministic in `seed`."""
+    rng = np.random.default_rng(seed)
+    v = ["[PAD]"] + ["[unused%d]" % i for i in range(99)] + ["[UNK]", "[CLS]", "[SEP]", "[MASK]"]
+    chars = [chr(c) for c in range(33, 127)] + [chr(c) for c in range(0xA1, 0x180) if chr(c).isprintable()]
+    chars += [chr(c) for c in range(0x391, 0x3CA)] + [chr(0x4E00 + int(i)) for i in rng.choice(20000, 600, False)]
+    chars += [chr(0x3000 + i) for i in range(1, 32)]
+    v += chars + ["##" + c for c in chars if c.isalnum()]
+    letters = np.array(list("etaoinshrdlcumwfgypbvkjxqz"))
+    freq = np.array([12.7, 9.1, 8.2, 7.5, 7.0, 6.7, 6.3, 6.1, 6.0, 4.3, 4.0, 2.8, 2.8, 2.4, 2.4, 2.2, 2.0, 2.0,
+                     1.9, 1.5, 1.0, 0.8, 0.2, 0.2, 0.1, 0.1])
+    freq = freq / freq.sum()
+    seen = set(v)
+
+    def word(lo, hi):
+        return "".join(rng.choice(letters, int(rng.integers(lo, hi + 1)), p=freq))
+    n_sub = 6000
+    while len(v) < n_vocab - n_sub:
+        w = word(2, 14)
+        if w not in seen or rng.random() < 0.002:    # rare duplicates: token_to_id keeps the first
+            seen.add(w)
+            v.append(w)
+    while len(v) < n_vocab:
+        w = "##" + word(1, 6)
+        if w not in seen or rng.random() < 0.002:    # subword_token_to_id keeps the last
+            seen.add(w)
+            v.append(w)
+    return v[:n_vocab]
+
+
+def bert_like_texts(vocab, n, n_words, seed=0):
+    """Texts over a bert_like_vocab: mostly whole words, words glued from a word and
+    '##' pieces (re-split by greedy longest-prefix matching), capitalised and accented
+    forms, unknown letter runs, numbers, punctuation attached to words, CJK runs,
+    2-4-byte characters outside the vocab, and irregular whitespace."""
+    rng = np.random.default_rng(seed)
+    whole = [w for w in vocab[104:] if w.isalpha() and not w.startswith("##") and len(w) > 1]
+    subs = [w[2:] for w in vocab if w.startswith("##") and len(w) > 3]
+    cjk = [w for w in vocab[104:] if len(w) == 1 and ord(w) >= 0x3400]
+    acc = ["café", "naïve", "Über", "ÉCOLE", "résumé", "Ångström", "façade"]
+    seps = [" ", " ", " ", " ", "  ", "\n", "\t", " \r\n "]
+    out = []
+    for _ in range(n):
+        parts = []
+        for _ in range(n_words):
+            r = rng.random()
+            if r < 0.55:
+                w = whole[int(rng.integers(len(whole)))]
+            elif r < 0.75:
+                w = whole[int(rng.integers(len(whole)))] + "".join(
+                    subs[int(rng.integers(len(subs)))] for _ in range(int(rng.integers(1, 3))))
+            elif r < 0.80:
+                w = whole[int(rng.integers(len(whole)))].capitalize()
+            elif r < 0.83:
+                w = acc[int(rng.integers(len(acc)))]
+            elif r < 0.87:
+                w = "".join(chr(int(c)) for c in rng.integers(97, 123, int(rng.integers(3, 16))))
+            elif r < 0.90:
+                w = str(int(rng.integers(0, 100000)))
+            elif r < 0.95:
+                w = rng.choice(["(", '"', "'"]) + whole[int(rng.integers(len(whole)))] + rng.choice([",", ".", "!", "?", ");", "'s"])
+            elif r < 0.98:
+                w = "".join(cjk[int(rng.integers(len(cjk)))] for _ in range(int(rng.integers(1, 5))))
+            else:
+                w = rng.choice(["\u00e9t\u00e9", "\U0001F600ok", "\u0416\u0437", "x\u2014y", "\uFF01", "a\u0301"])
+            parts.append(str(w))
+            parts.append(seps[int(rng.integers(len(seps)))])
+        out.append("".join(parts).encode("utf-8"))
+    return out
+
+
 def outlier_channels(d, seed=1234):
     """The residual-stream channels the "sharp" profile drives to |x| ~ 50-200."""
     return np.sort(np.random.default_rng(seed + 1).choice(d, 3, replace=False))

@@ -3,7 +3,10 @@
 // `char` (bytes >= 0x80 are never punctuation or space there).
 #include "tokenizer.h"
 
+#include <algorithm>
 #include <cstring>
+#include <vector>
+#include <utility>
 
 namespace emb {
 
@@ -64,24 +67,11 @@ void Vocab::Trie::init(size_t expected)
     keys.assign(cap, 0);
     child.assign(cap, 0);
     term.assign(1, -1);
-    for (int32_t &r : root) r = -1;
     n_nodes = 1;
-}
-
-int32_t Vocab::Trie::step(int32_t node, uint8_t b) const
-{
-    const uint64_t k = (((uint64_t)node << 8) | b) + 1;
-    size_t i = mix(k) & (keys.size() - 1);
-    for (;;) {
-        if (keys[i] == 0) return -1;
-        if (keys[i] == k) return child[i];
-        i = (i + 1) & (keys.size() - 1);
-    }
 }
 
 int32_t Vocab::Trie::add_child(int32_t node, uint8_t b)
 {
-    if (node == 0 && root[b] >= 0) return root[b];
     const uint64_t k = (((uint64_t)node << 8) | b) + 1;
     if ((size_t)n_nodes * 2 >= keys.size()) {     // grow
         std::vector<uint64_t> ok;
@@ -104,7 +94,6 @@ int32_t Vocab::Trie::add_child(int32_t node, uint8_t b)
             keys[i] = k;
             child[i] = n_nodes;
             term.push_back(-1);
-            if (node == 0) root[b] = n_nodes;
             return n_nodes++;
         }
         if (keys[i] == k) return child[i];
@@ -112,24 +101,107 @@ int32_t Vocab::Trie::add_child(int32_t node, uint8_t b)
     }
 }
 
-void Vocab::Trie::insert(const char *s, size_t n, int32_t id, bool overwrite)
+bool Vocab::Trie::insert(const char *s, size_t n, int32_t id, bool overwrite)
 {
     int32_t node = 0;
     for (size_t i = 0; i < n; ++i) node = add_child(node, (uint8_t)s[i]);
-    if (term[(size_t)node] < 0 || overwrite) term[(size_t)node] = id;
+    if (term[(size_t)node] < 0 || overwrite) {
+        term[(size_t)node] = id;
+        return true;
+    }
+    return false;
+}
+
+void Vocab::Trie::freeze()
+{
+    const size_t N = (size_t)n_nodes;
+    // the edges grouped by parent (counting sort), bytes ascending within a parent
+    std::vector<int32_t> cnt(N + 1, 0);
+    for (size_t j = 0; j < keys.size(); ++j)
+        if (keys[j]) ++cnt[(size_t)((keys[j] - 1) >> 8) + 1];
+    for (size_t v = 0; v < N; ++v) cnt[v + 1] += cnt[v];
+    std::vector<std::pair<uint8_t, int32_t>> adj((size_t)cnt[N]);
+    std::vector<int32_t> fill(cnt.begin(), cnt.end() - 1);
+    for (size_t j = 0; j < keys.size(); ++j)
+        if (keys[j]) {
+            const size_t p = (size_t)((keys[j] - 1) >> 8);
+            adj[(size_t)fill[p]++] = {(uint8_t)((keys[j] - 1) & 0xff), child[j]};
+        }
+    for (size_t v = 0; v < N; ++v) std::sort(adj.begin() + cnt[v], adj.begin() + cnt[v + 1]);
+    // double array, nodes placed breadth-first: each node's children go to the
+    // first base b with every slot b + byte free (first-fit from the lowest free
+    // slot); slot 0 is the root, check = parent slot, -1 = free
+    std::vector<int32_t> pos(N, -1);   // node -> slot
+    da.assign(N + 512, Slot{0, -1});
+    std::vector<int32_t> sterm(da.size(), -1);
+    std::vector<uint8_t> used(da.size(), 0), base_used(da.size(), 0);
+    auto ensure = [&](size_t n) {
+        if (n > da.size()) {
+            const size_t m = std::max(n, da.size() * 3 / 2);
+            da.resize(m, Slot{0, -1});
+            sterm.resize(m, -1);
+            used.resize(m, 0);
+            base_used.resize(m, 0);
+        }
+    };
+    pos[0] = 0;
+    used[0] = 1;
+    da[0].check = 0;
+    size_t first_free = 1;
+    std::vector<int32_t> queue;
+    queue.reserve(N);
+    queue.push_back(0);
+    for (size_t h = 0; h < queue.size(); ++h) {
+        const int32_t v = queue[h];
+        const int32_t sv = pos[(size_t)v];
+        sterm[(size_t)sv] = term[(size_t)v];
+        const int32_t e0 = cnt[(size_t)v], e1 = cnt[(size_t)v + 1];
+        if (e0 == e1) continue;
+        while (first_free < used.size() && used[first_free]) ++first_free;
+        const int32_t c0 = adj[(size_t)e0].first;
+        // base candidates: the first child lands on a free slot at or past first_free
+        for (int64_t b = std::max<int64_t>(1, (int64_t)first_free - c0);; ++b) {
+            ensure((size_t)b + 256);
+            if (base_used[(size_t)b] || used[(size_t)(b + c0)]) continue;
+            bool ok = true;
+            for (int32_t e = e0 + 1; e < e1 && ok; ++e) ok = !used[(size_t)(b + adj[(size_t)e].first)];
+            if (!ok) continue;
+            base_used[(size_t)b] = 1;      // distinct bases: a slot's check names one parent
+            da[(size_t)sv].base = (int32_t)b;
+            for (int32_t e = e0; e < e1; ++e) {
+                const size_t slot = (size_t)(b + adj[(size_t)e].first);
+                used[slot] = 1;
+                da[slot].check = sv;
+                pos[(size_t)adj[(size_t)e].second] = (int32_t)slot;
+                queue.push_back(adj[(size_t)e].second);
+            }
+            break;
+        }
+    }
+    size_t last = 0;
+    for (size_t i = 0; i < used.size(); ++i)
+        if (used[i]) last = i;
+    da.resize(last + 257, Slot{0, -1});   // every base + byte stays in range
+    sterm.resize(da.size(), -1);
+    for (size_t i = 0; i < da.size(); ++i)
+        if (sterm[i] >= 0) da[i].base |= kTerm;
+    da_term.swap(sterm);
+    std::vector<uint64_t>().swap(keys);
+    std::vector<int32_t>().swap(child);
+    std::vector<int32_t>().swap(term);
 }
 
 size_t Vocab::Trie::longest(const char *s, size_t n, int32_t *id) const
 {
-    if (n == 0) return 0;
-    int32_t node = root[(uint8_t)s[0]];
-    if (node < 0) return 0;
+    const Slot *d = da.data();
+    int32_t cur = 0, base = d[0].base & ~kTerm;
     size_t best = 0;
-    if (term[(size_t)node] >= 0) { best = 1; *id = term[(size_t)node]; }
-    for (size_t i = 1; i < n; ++i) {
-        node = step(node, (uint8_t)s[i]);
-        if (node < 0) break;
-        if (term[(size_t)node] >= 0) { best = i + 1; *id = term[(size_t)node]; }
+    for (size_t i = 0; i < n; ++i) {
+        const int32_t nx = base + (uint8_t)s[i];
+        if (d[nx].check != cur || nx == 0) break;
+        cur = nx;
+        base = d[cur].base;
+        if (base & kTerm) { best = i + 1; base &= ~kTerm; *id = da_term[(size_t)cur]; }
     }
     return best;
 }
@@ -148,17 +220,15 @@ void Vocab::build(const std::vector<std::string> &tokens)
             sub_.insert(w.data() + 2, w.size() - 2, (int32_t)i, /*overwrite=*/true);
             has_sub_[i] = 1;
         }
-        int32_t tmp;
         // first occurrence wins; the empty string is a key too (never looked up)
         if (w.empty()) {
             if (!empty_seen) { has_whole_[i] = 1; empty_seen = true; }
             continue;
         }
-        if (whole_.longest(w.data(), w.size(), &tmp) != w.size()) {
-            whole_.insert(w.data(), w.size(), (int32_t)i, false);
-            has_whole_[i] = 1;
-        }
+        if (whole_.insert(w.data(), w.size(), (int32_t)i, false)) has_whole_[i] = 1;
     }
+    whole_.freeze();
+    sub_.freeze();
 }
 
 const char *Vocab::id_to_token(int32_t id) const
@@ -173,37 +243,52 @@ int32_t Vocab::tokenize(const char *text, int32_t n_max_tokens, int32_t *out, in
     const uint8_t *in = (const uint8_t *)text;
     const size_t n_in = std::strlen(text);
 
-    // 1) accent strip + A-Z lowercase at character starts (bert.cpp:206-251);
-    // per-thread scratch strings keep their capacity across calls
-    thread_local std::string a, b;
-    a.clear();
-    a.reserve(n_in);
+    // 1) accent strip + A-Z lowercase at character starts (bert.cpp:206-251), one
+    // pass: a character's first byte is the only place an ASCII letter can be
+    // lowered (bytes inside a malformed multi-byte span are copied raw, as the
+    // reference's char-stride loop leaves them); per-thread scratch buffers
+    thread_local std::vector<char> abuf, bbuf;
+    if (abuf.size() < n_in + 1) abuf.resize(n_in + 1);
+    char *a = abuf.data();
+    size_t na = 0;
     for (size_t i = 0; i < n_in;) {
-        const size_t len = (size_t)lead_len(in[i]);
+        const uint8_t c = in[i];
+        if (c < 0x80) {
+            a[na++] = (char)(c >= 'A' && c <= 'Z' ? c - 'A' + 'a' : c);
+            ++i;
+            continue;
+        }
+        const size_t len = (size_t)lead_len(c);
         const size_t take = i + len <= n_in ? len : n_in - i;
-        if (take == 2 && in[i] == 0xC3 && kAccents.map[in[i + 1]]) a.push_back(kAccents.map[in[i + 1]]);
-        else a.append((const char *)in + i, take);
+        if (take == 2 && c == 0xC3 && kAccents.map[in[i + 1]]) {
+            const char m = kAccents.map[in[i + 1]];
+            a[na++] = (char)(m >= 'A' && m <= 'Z' ? m - 'A' + 'a' : m);
+        } else {
+            for (size_t k = 0; k < take; ++k) a[na++] = (char)in[i + k];
+        }
         i += take;
     }
-    for (size_t i = 0; i < a.size(); i += (size_t)lead_len((uint8_t)a[i]))
-        if (a[i] >= 'A' && a[i] <= 'Z') a[i] = (char)(a[i] - 'A' + 'a');
 
-    // 2) isolate ASCII punctuation and 3-byte CJK (bert.cpp:317-339),
-    // 3) whitespace split (bert.cpp:341-358) -- fused: collect word spans.
-    b.clear();
-    b.reserve(a.size() * 2 + 8);
-    const uint8_t *pa = (const uint8_t *)a.data();
-    for (size_t i = 0; i < a.size();) {
-        const int len = lead_len(pa[i]);
-        if (len == 1 && is_punct(pa[i])) {
-            b.push_back(' '); b.push_back((char)pa[i]); b.push_back(' ');
-            i += 1;
-        } else if (len == 3 && is_cjk3(pa + i, a.size() - i)) {
-            b.push_back(' '); b.append((const char *)pa + i, 3); b.push_back(' ');
+    // 2) isolate ASCII punctuation and 3-byte CJK (bert.cpp:317-339), byte by
+    // byte over the normalised text as the reference walks it
+    if (bbuf.size() < 3 * na + 8) bbuf.resize(3 * na + 8);
+    char *b = bbuf.data();
+    size_t nbb = 0;
+    const uint8_t *pa = (const uint8_t *)a;
+    for (size_t i = 0; i < na;) {
+        const uint8_t c = pa[i];
+        if (c < 0x80) {
+            if (is_punct(c)) { b[nbb] = ' '; b[nbb + 1] = (char)c; b[nbb + 2] = ' '; nbb += 3; }
+            else b[nbb++] = (char)c;
+            ++i;
+        } else if (lead_len(c) == 3 && is_cjk3(pa + i, na - i)) {
+            b[nbb] = ' '; b[nbb + 1] = (char)c; b[nbb + 2] = (char)pa[i + 1]; b[nbb + 3] = (char)pa[i + 2];
+            b[nbb + 4] = ' ';
+            nbb += 5;
             i += 3;
         } else {
-            b.push_back((char)pa[i]);
-            i += 1;
+            b[nbb++] = (char)c;
+            ++i;
         }
     }
 
@@ -211,8 +296,8 @@ int32_t Vocab::tokenize(const char *text, int32_t n_max_tokens, int32_t *out, in
     int32_t t = 0;
     auto emit = [&](int32_t id) { if (t < cap) out[t] = id; ++t; };
     emit(101);
-    const char *pb = b.data();
-    const size_t nb = b.size();
+    const char *pb = b;
+    const size_t nb = nbb;
     size_t l = 0;
     for (size_t r = 0; r <= nb; ++r) {
         if (r < nb && !is_space((uint8_t)pb[r])) continue;

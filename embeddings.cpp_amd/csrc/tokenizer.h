@@ -28,16 +28,26 @@ public:
 
 private:
     struct Trie {
-        // node -> (byte -> child) in a flat open-addressing table
+        // construction: node -> (byte -> child) in a flat open-addressing table
         std::vector<uint64_t> keys;   // (node << 8 | byte) + 1, 0 = empty
         std::vector<int32_t> child;
         std::vector<int32_t> term;    // node -> token id or -1
-        int32_t root[256];            // the root's children, dense (every word's first byte)
         int32_t n_nodes = 1;
         void init(size_t expected);
-        int32_t step(int32_t node, uint8_t b) const;
         int32_t add_child(int32_t node, uint8_t b);
-        void insert(const char *s, size_t n, int32_t id, bool overwrite);
+        // stores id at the key unless one is there and !overwrite; true if stored
+        bool insert(const char *s, size_t n, int32_t id, bool overwrite);
+        // lookups: freeze() turns the trie into a double array (base/check, one
+        // 8-byte slot per node, nodes placed in breadth-first order so the hot
+        // upper levels share cache lines): a step is slot[base[s] + byte] with
+        // check == s, one memory access; slots holding a token carry a flag bit
+        // and their id sits in a side array.  The construction table's hash
+        // probes cost one DRAM miss per byte on a 30k-entry vocab.
+        struct Slot { int32_t base; int32_t check; };   // base | kTerm if the slot ends a token
+        static constexpr int32_t kTerm = 1 << 30;
+        std::vector<Slot> da;         // da[0] = root
+        std::vector<int32_t> da_term; // slot -> token id (where flagged)
+        void freeze();
         // length of the longest key that is a prefix of s[0..n), 0 if none
         size_t longest(const char *s, size_t n, int32_t *id) const;
     };

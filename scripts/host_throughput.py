@@ -1,23 +1,23 @@
 #!/usr/bin/env python3
 """Host-side throughput of the two SURVEY §8(f) rows around the GPU forward.
 
-  tok     (f2, CPU only) WordPiece tokenization of ~508-token texts: the reference's
-          own tokenizer source (bert.cpp:195-417 compiled into oracle/_ref/libreftok.so
-          by oracle/build_ref.sh -- std::map substring probes, one thread, as
-          bert_encode_batch runs it, bert.cpp:1402-1406) against libbert's trie
-          tokenizer (csrc/tokenizer.cpp) on 1 thread and on 8 / 16 threads (ctypes
-          drops the GIL, so Python threads run the C tokenizer in parallel).  Token
-          ids of both are compared on every text.
+  tok     (f2, CPU only) WordPiece tokenization of ~500-token texts over a
+          30,522-entry BERT-size vocab: the reference's own tokenizer source
+          (bert.cpp:195-417 compiled into oracle/_ref/libreftok.so by
+          oracle/build_ref.sh -- std::map substring probes, one thread, as
+          bert_encode_batch runs it, bert.cpp:1402-1406) against the library's own
+          batch stage bertx_tokenize_batch (csrc/tokenizer.cpp trie on the persistent
+          pool, csrc/task_pool.cpp) at 1 / 8 / 16 threads.  Token ids of both are
+          compared on every text the reference tokenizes.
   server  (f3, GPU) requests/s of the TCP protocol (examples/server.cpp: int32 n_embd
           on connect, one text per recv, n_embd float32 back) with 1 / 8 / 64
           concurrent clients: build/bin/server (micro-batching) against the
           reference's own examples/server.cpp linked to libbert.so
           (build/ref_clients/server: one client at a time, one text per forward).
 
-Prints one JSON object per measurement.  Vocab: the 692-entry BERT word-piece vocab
-of the committed fixtures (tests/golden/tokenizer_cases.json); server model: the
-bench's synthetic bge-base-en-v1.5 q4_0 (words w<i> are single tokens, so a text
-of k words is exactly k + 2 tokens).
+Prints one JSON object per measurement.  Server model: the bench's synthetic
+bge-base-en-v1.5 q4_0 (words w<i> are single tokens, so a text of k words is
+exactly k + 2 tokens).
 """
 import argparse
 import ctypes
@@ -66,27 +66,29 @@ def make_texts(vocab, n, n_words, seed=0):
 
 
 def cmd_tok(a):
-    vocab = json.load(open(os.path.join(ROOT, "tests", "golden", "tokenizer_cases.json")))["vocab"]
+    """Tokenizer throughput at BERT's vocabulary size: 30,522 WordPiece entries
+    (bertpy.bert_like_vocab) and ~500-token texts (bertpy.bert_like_texts); the
+    reference's tokenizer source on one thread (as bert_encode_batch runs it,
+    bert.cpp:1402-1406) against the library's own batch stage, bertx_tokenize_batch
+    -- the function bert_encode_batch calls -- on 1 / 8 / 16 threads of its
+    persistent pool, one call over all texts, timed around that call."""
+    vocab = bertpy.bert_like_vocab(30522, seed=0)
     n_max = 512
-    # size the texts to ~508 tokens with the library tokenizer itself
+    hp = dict(n_vocab=len(vocab), n_max_tokens=n_max, n_embd=64, n_intermediate=128, n_head=1, n_layer=1)
+    path = os.path.join("/tmp", "host_tok_bertvocab.bin")
+    bertpy.write_model(path, hp, vocab, bertpy.synthetic_tensors(hp, seed=1), 0)
     os.environ["BERT_HOST_ONLY"] = "1"
     lib = bertpy.load_lib()
-    m = bertpy.BertModel(os.path.join(ROOT, "tests", "golden", "tiny32", "ggml-model-f32.bin"), lib=lib)
-    probe = make_texts(vocab, 4, 200, seed=1)
+    m = bertpy.BertModel(path, lib=lib)
+    probe = bertpy.bert_like_texts(vocab, 8, 200, seed=1)
     per_word = np.mean([m.tokenize(t, 100000)[1] for t in probe]) / 200
-    texts = make_texts(vocab, a.texts, int(506 / per_word), seed=2)
-    cap = 4 * n_max
-    buf = (ctypes.c_int32 * cap)()
-    n = ctypes.c_int32()
-
-    def ours(t, bb, nn):
-        lib.bert_tokenize(m.ctx, t, bb, ctypes.byref(nn), n_max)
-        return nn.value
-
-    lens = [ours(t, buf, n) for t in texts]
-    emit(kind="texts", n=len(texts), mean_tokens=float(np.mean(lens)), min_tokens=int(min(lens)),
-         max_tokens=int(max(lens)))
-
+    texts = bertpy.bert_like_texts(vocab, a.texts, int(500 / per_word), seed=2)
+    arr = (ctypes.c_char_p * len(texts))(*texts)
+    ids = np.zeros((len(texts), n_max), np.int32)
+    lens = np.zeros(len(texts), np.int32)
+    assert lib.bertx_tokenize_batch(m.ctx, 1, len(texts), arr, n_max, ids.ctypes.data, lens.ctypes.data) == 0
+    emit(kind="texts", n=len(texts), vocab=len(vocab), mean_tokens=float(np.mean(lens)), min_tokens=int(lens.min()),
+         max_tokens=int(lens.max()), mean_bytes=float(np.mean([len(t) for t in texts])))
     res = {}
     ref_path = os.path.join(ROOT, "oracle", "_ref", "libreftok.so")
     if os.path.exists(ref_path):
@@ -99,41 +101,30 @@ def cmd_tok(a):
         for i, v in enumerate(vocab):
             b = v.encode()
             R.reftok_add(rc, b, len(b), i)
-        rbuf = (ctypes.c_int32 * cap)()
-        # ids equal on every text (the written prefix)
-        for t in texts[:200]:
-            ours(t, buf, n)
-            rn = ctypes.c_int32()
-            R.reftok_tokenize(rc, t, rbuf, ctypes.byref(rn), n_max)
-            assert rn.value == n.value and list(rbuf[:min(n.value, n_max)]) == list(buf[:min(n.value, n_max)])
+        rbuf = (ctypes.c_int32 * (4 * n_max))()
+        nref = min(len(texts), a.ref_texts)
         t0 = time.perf_counter()
-        for t in texts:
+        for i, t in enumerate(texts[:nref]):
             rn = ctypes.c_int32()
             R.reftok_tokenize(rc, t, rbuf, ctypes.byref(rn), n_max)
+            # ids equal on every text timed (the written prefix)
+            assert rn.value == lens[i] and list(rbuf[:min(rn.value, n_max)]) == list(ids[i, :min(lens[i], n_max)])
         el = time.perf_counter() - t0
-        res["reference"] = len(texts) / el
-        emit(kind="tokenizer", impl="reference bert.cpp:195-417 (std::map)", threads=1, texts_per_s=round(len(texts) / el, 1),
-             us_per_text=round(el / len(texts) * 1e6, 2))
+        res["reference"] = nref / el
+        emit(kind="tokenizer", impl="reference bert.cpp:195-417 (std::map), 30,522-entry vocab", threads=1,
+             texts=nref, texts_per_s=round(nref / el, 1), us_per_text=round(el / nref * 1e6, 2))
     for thr in a.threads:
-        chunks = [texts[i::thr] for i in range(thr)]
-
-        def work(ch):
-            bb = (ctypes.c_int32 * cap)()
-            nn = ctypes.c_int32()
-            for t in ch:
-                ours(t, bb, nn)
-
-        ths = [threading.Thread(target=work, args=(c,)) for c in chunks]
-        t0 = time.perf_counter()
-        for th in ths:
-            th.start()
-        for th in ths:
-            th.join()
-        el = time.perf_counter() - t0
-        res[thr] = len(texts) / el
-        emit(kind="tokenizer", impl="libbert trie (csrc/tokenizer.cpp)", threads=thr,
-             texts_per_s=round(len(texts) / el, 1), us_per_text_per_thread=round(el * thr / len(texts) * 1e6, 2),
-             vs_reference_1thread=round(res[thr] / res["reference"], 2) if "reference" in res else None)
+        best = 0.0
+        for _ in range(3):
+            t0 = time.perf_counter()
+            assert lib.bertx_tokenize_batch(m.ctx, thr, len(texts), arr, n_max, ids.ctypes.data,
+                                            lens.ctypes.data) == 0
+            best = max(best, len(texts) / (time.perf_counter() - t0))
+        res[thr] = best
+        emit(kind="tokenizer", impl="libbert bertx_tokenize_batch (trie, persistent pool)", threads=thr,
+             texts=len(texts), texts_per_s=round(best, 1), us_per_text_per_thread=round(thr / best * 1e6, 2),
+             vs_reference_1thread=round(best / res["reference"], 2) if "reference" in res else None,
+             cpus_visible=len(os.sched_getaffinity(0)))
 
 
 def recv_exact(sock, n):
@@ -227,10 +218,11 @@ def main():
     t = sub.add_parser("tok")
     t.add_argument("--texts", type=int, default=2000)
     t.add_argument("--threads", type=int, nargs="+", default=[1, 8, 16])
+    t.add_argument("--ref-texts", type=int, default=400, help="texts timed through the reference tokenizer")
     s = sub.add_parser("server")
     s.add_argument("--clients", type=int, nargs="+", default=[1, 8, 64])
     s.add_argument("--words", type=int, default=126)
-    s.add_argument("--min-requests", type=int, default=512)
+    s.add_argument("--min-requests", type=int, default=5000)
     s.add_argument("--wait-us", type=int, default=2000)
     a = p.parse_args()
     cmd_tok(a) if a.cmd == "tok" else cmd_server(a)
