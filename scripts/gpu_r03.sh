@@ -8,7 +8,7 @@ TAG=${TAG:-r03a}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp PARITY_LOG=$OUT/parity.jsonl
-STEPS=${STEPS:-"test bench prof"}
+STEPS=${STEPS:-"test bench prof tok"}
 TESTS=${TESTS:-tests}
 has() { [[ " $STEPS " == *" $1 "* ]]; }
 step() { local lim=$1; shift; timeout -k 10 $lim "$@"; }
