@@ -13,7 +13,7 @@ TESTS=${TESTS:-tests}
 has() { [[ " $STEPS " == *" $1 "* ]]; }
 step() { local lim=$1; shift; timeout -k 10 $lim "$@"; }
 if has test; then
-  step 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu $TESTS > $OUT/gputest.log 2>&1 || { tail -40 $OUT/gputest.log; exit 1; }
+  step 900 python -u -m pytest ${PYX:--x} -q -rf --timeout 300 --timeout-method thread -m gpu $TESTS > $OUT/gputest.log 2>&1 || { tail -40 $OUT/gputest.log; exit 1; }
   tail -3 $OUT/gputest.log
 fi
 if has bench; then
@@ -26,6 +26,12 @@ fi
 if has inproc; then
   BERT_DEVICES=0,0,0,0,0,0,0,0 step 600 python -u bench.py --inproc --gpus 8 --steps 5 --warmup 1 > $OUT/inproc.log 2>&1 || { tail -20 $OUT/inproc.log; exit 1; }
   BERT_DEVICES=0 step 600 python -u bench.py --inproc --gpus 1 --steps 5 --warmup 1 >> $OUT/inproc.log 2>&1 || { tail -20 $OUT/inproc.log; exit 1; }
+fi
+if has gemmab; then
+  # weight formats and tile configs of the C3 GEMM forms on random operands
+  for f in 1 2; do SWEEP_FMT=$f step 120 python -u scripts/gemm_one.py all 0 20 >> $OUT/gemmab.log 2>&1 || exit 1; done
+  SWEEP_FMT=2 step 120 python -u scripts/gemm_one.py all 5 20 >> $OUT/gemmab.log 2>&1 || exit 1
+  cat $OUT/gemmab.log
 fi
 if has tok; then step 300 python -u scripts/host_throughput.py tok --texts 4000 > $OUT/tok.log 2>&1 || exit 1; fi
 if has server; then step 400 python -u scripts/host_throughput.py server > $OUT/server.log 2>&1 || { tail -20 $OUT/server.log; exit 1; }; fi
