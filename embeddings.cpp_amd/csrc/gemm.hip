@@ -407,6 +407,17 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
             if (ks + 2 < KS) kstep(w2, w1, ks + 2);
         }
     }
+    // Every weight load the counts assume must be issued.  The tail steps' loads
+    // (clamped to the last K-step) feed no later step, so without a use hipcc
+    // deletes them as dead -- and a tail step's back wait, counted with those
+    // loads behind X(ks + 1), then leaves the last LQ pieces of X(ks + 1) in
+    // flight across the barrier (the NS 2 ring with KS % 3 == 2, the 4-set ring
+    // with KS % 4 == 2: the round-2 "4-set ring race").  An asm use of every set
+    // here keeps them live; it waits only for loads the epilogue would wait for.
+    w0.pin_all();
+    w1.pin_all();
+    w2.pin_all();
+    if constexpr (WR == 4) w3.pin_all();
     wait_vmcnt<0>();
     ZSTAMP(2, __builtin_amdgcn_s_memtime());
 #ifdef GEMM_STAMPS
