@@ -137,7 +137,38 @@ def recv_exact(sock, n):
     return b
 
 
+def _client_proc(port, n_threads, per_client, text, q):
+    """One load-generator process: n_threads clients, each sending per_client texts
+    and reading the n_embd-float replies; reports (latencies, errors, cpu seconds)."""
+    errors, lat = [], []
+
+    def client():
+        try:
+            with socket.create_connection(("127.0.0.1", port), timeout=300) as s:
+                nd = struct.unpack("i", recv_exact(s, 4))[0]
+                for _ in range(per_client):
+                    t0 = time.perf_counter()
+                    s.sendall(text)
+                    recv_exact(s, 4 * nd)
+                    lat.append(time.perf_counter() - t0)
+        except Exception as e:  # noqa: BLE001 -- reported
+            errors.append(repr(e))
+
+    c0 = os.times()
+    ths = [threading.Thread(target=client) for _ in range(n_threads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(600)
+    c1 = os.times()
+    q.put((lat, errors, (c1.user - c0.user) + (c1.system - c0.system)))
+
+
 def run_server_load(exe_args, port, n_clients, per_client, text, env):
+    """Clients spread over up to 16 load-generator processes (a single Python process
+    is GIL-bound long before the server is); returns (requests/s, median latency,
+    the generator's CPU use as a fraction of its processes' wall time)."""
+    import multiprocessing as mp
     proc = subprocess.Popen(exe_args, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, env=env)
     try:
         for _ in range(1200):
@@ -148,31 +179,24 @@ def run_server_load(exe_args, port, n_clients, per_client, text, env):
                 if proc.poll() is not None:
                     raise RuntimeError(f"server exited {proc.returncode}")
                 time.sleep(0.1)
-        errors = []
-        lat = []
-
-        def client():
-            try:
-                with socket.create_connection(("127.0.0.1", port), timeout=300) as s:
-                    nd = struct.unpack("i", recv_exact(s, 4))[0]
-                    for _ in range(per_client):
-                        t0 = time.perf_counter()
-                        s.sendall(text)
-                        recv_exact(s, 4 * nd)
-                        lat.append(time.perf_counter() - t0)
-            except Exception as e:  # noqa: BLE001 -- reported
-                errors.append(repr(e))
-
-        ths = [threading.Thread(target=client) for _ in range(n_clients)]
+        n_proc = min(16, n_clients)
+        per_proc = [n_clients // n_proc + (1 if i < n_clients % n_proc else 0) for i in range(n_proc)]
+        ctx = mp.get_context("fork")
+        q = ctx.Queue()
+        ps = [ctx.Process(target=_client_proc, args=(port, k, per_client, text, q)) for k in per_proc]
         t0 = time.perf_counter()
-        for th in ths:
-            th.start()
-        for th in ths:
-            th.join(600)
+        for p_ in ps:
+            p_.start()
+        res = [q.get(timeout=900) for _ in ps]
         el = time.perf_counter() - t0
+        for p_ in ps:
+            p_.join(60)
+        errors = [e for r in res for e in r[1]]
         if errors:
             raise RuntimeError(errors[:3])
-        return n_clients * per_client / el, float(np.median(lat))
+        lat = [x for r in res for x in r[0]]
+        cpu = sum(r[2] for r in res) / (el * n_proc)
+        return n_clients * per_client / el, float(np.median(lat)), cpu
     finally:
         proc.kill()
         proc.wait(timeout=30)
@@ -195,10 +219,11 @@ def cmd_server(a):
         with socket.socket() as s:
             s.bind(("127.0.0.1", 0))
             port = s.getsockname()[1]
-        rps, med = run_server_load([ours, "-m", path, "--port", str(port), "--max-batch", "64", "--wait-us",
-                                    str(a.wait_us)], port, n_cli, per, text, env)
+        rps, med, cpu = run_server_load([ours, "-m", path, "--port", str(port), "--max-batch", "64", "--wait-us",
+                                         str(a.wait_us)], port, n_cli, per, text, env)
         emit(kind="server", impl="build/bin/server (micro-batching)", clients=n_cli, tokens_per_text=a.words + 2,
-             requests=n_cli * per, requests_per_s=round(rps, 1), median_latency_ms=round(med * 1e3, 3))
+             requests=n_cli * per, requests_per_s=round(rps, 1), median_latency_ms=round(med * 1e3, 3),
+             client_cpu_frac=round(cpu, 3), client_bound=bool(cpu > 0.9))
         if os.path.exists(ref) and n_cli == 1:
             # the reference server takes one client at a time (backlog 1, serial accept
             # loop, examples/server.cpp:92-118): concurrent clients queue behind each
@@ -206,10 +231,10 @@ def cmd_server(a):
             with socket.socket() as s:
                 s.bind(("127.0.0.1", 0))
                 port = s.getsockname()[1]
-            rps, med = run_server_load([ref, "-m", path, "--port", str(port)], port, n_cli, per, text, env)
+            rps, med, cpu = run_server_load([ref, "-m", path, "--port", str(port)], port, n_cli, per, text, env)
             emit(kind="server", impl="reference examples/server.cpp on libbert (batch 1 per recv)", clients=n_cli,
                  tokens_per_text=a.words + 2, requests=n_cli * per, requests_per_s=round(rps, 1),
-                 median_latency_ms=round(med * 1e3, 3))
+                 median_latency_ms=round(med * 1e3, 3), client_cpu_frac=round(cpu, 3))
 
 
 def main():
@@ -220,7 +245,7 @@ def main():
     t.add_argument("--threads", type=int, nargs="+", default=[1, 8, 16])
     t.add_argument("--ref-texts", type=int, default=400, help="texts timed through the reference tokenizer")
     s = sub.add_parser("server")
-    s.add_argument("--clients", type=int, nargs="+", default=[1, 8, 64])
+    s.add_argument("--clients", type=int, nargs="+", default=[1, 8, 32, 64])
     s.add_argument("--words", type=int, default=126)
     s.add_argument("--min-requests", type=int, default=5000)
     s.add_argument("--wait-us", type=int, default=2000)

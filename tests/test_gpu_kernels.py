@@ -137,14 +137,14 @@ def test_f32_gemm_matches_numpy(lib, epi, N, K, M):
         x16 = acc.astype(np.float16)
         assert np.array_equal(out.astype(np.float16).astype(np.float32), out)   # f16 values, as the table holds
         got = out.astype(np.float16)
-        ok = np.zeros(out.shape, bool)
-        for xin in (x16, np.nextafter(x16, np.float16(-np.inf)), np.nextafter(x16, np.float16(np.inf))):
-            t = table[xin.view(np.uint16)]
-            for cand in (t, np.nextafter(t, np.float16(-np.inf)), np.nextafter(t, np.float16(np.inf))):
-                ok |= got == cand
-        assert ok.all(), [(acc[i, j], got[i, j], table[x16[i, j:j + 1].view(np.uint16)][0])
-                          for i, j in np.argwhere(~ok)[:5]]
-        assert np.mean(got != table[x16.view(np.uint16)]) < 1e-2
+        ref = table[x16.view(np.uint16)].astype(np.float64)
+        # the f32 sum is within delta = 4e-7 sum|x w| of the f64 one (near-cancelling
+        # sums: many f16 steps of a subnormal result), GELU's slope is at most 1.13, and
+        # the table rounds to f16 on both sides of that
+        delta = 4e-7 * mag
+        ulp = np.spacing(np.abs(ref).astype(np.float16)).astype(np.float64)
+        assert np.all(np.abs(out - ref) <= 1.2 * delta + 2 * ulp + 1e-12)
+        assert np.mean(got != ref.astype(np.float16)) < 1e-2
     else:
         ref = acc + (R if epi == 2 else 0.0)
         assert np.all(np.abs(out - ref) <= 4e-7 * (mag + np.abs(R if epi == 2 else 0.0)) + 1e-30)
