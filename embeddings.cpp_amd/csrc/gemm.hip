@@ -631,6 +631,24 @@ void launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, 
     else dispatch_z<FMT, 2, 64, 4>(W, x, M, bias, epi, res, out, s, ln, lnf);
 }
 
+// Weight expansion to the f16 lane-order layout (kernels.h): each lane record's
+// four A fragments exactly as the GEMM's in-register dequantization produces
+// them (ZRegs<FMT>::frag), so a GEMM on the expanded copy gives the bits of the
+// fused one.  One thread per lane record.
+template <int FMT>
+__global__ __launch_bounds__(256) void expand_f16_kernel(DevWeight W, uint4 *__restrict__ dst, int n_rec)
+{
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= n_rec) return;
+    const int G = W.N / 32;
+    const int lane = r & 63, grp = (r >> 6) % G, ks = (r >> 6) / G, fr = lane & 15;
+    ZRegs<FMT> z;
+    z.load((const uint8_t *)W.qs + (size_t)r * ZRegs<FMT>::QB, W.d + (((size_t)ks * G + grp) * 16 + fr) * 4,
+           FMT == FMT_Q4_1 ? W.m + (((size_t)ks * G + grp) * 16 + fr) * 4 : nullptr);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) dst[(size_t)r * 4 + u] = __builtin_bit_cast(uint4, z.frag(u));
+}
+
 }  // namespace
 
 thread_local int g_gemm_cfg = 0;
@@ -660,6 +678,24 @@ extern "C" __attribute__((visibility("default"))) int bertx_gemm_stamps(unsigned
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gemm_stamps), n * 8) == hipSuccess ? 0 : -1;
 }
 #endif
+
+int launch_expand_f16(const DevWeight &W, void *dst, hipStream_t s, DevWeight &out)
+{
+    if (W.N % 32 || W.K % ZK || W.kx) return -1;
+    const int n_rec = (W.K / ZK) * (W.N / 32) * 64, grid = (n_rec + 255) / 256;
+    switch (W.fmt) {
+    case FMT_Q4_0: expand_f16_kernel<FMT_Q4_0><<<grid, 256, 0, s>>>(W, (uint4 *)dst, n_rec); break;
+    case FMT_Q4_1: expand_f16_kernel<FMT_Q4_1><<<grid, 256, 0, s>>>(W, (uint4 *)dst, n_rec); break;
+    case FMT_Q8_0: expand_f16_kernel<FMT_Q8_0><<<grid, 256, 0, s>>>(W, (uint4 *)dst, n_rec); break;
+    default: return -1;
+    }
+    out = DevWeight();
+    out.fmt = FMT_F16;
+    out.N = W.N;
+    out.K = W.K;
+    out.qs = dst;
+    return 0;
+}
 
 int launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi, const void *res,
                 void *out, hipStream_t s, const LnFold &ln)

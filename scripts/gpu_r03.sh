@@ -30,6 +30,16 @@ if has inproc; then
   BERT_DEVICES=0,0,0,0,0,0,0,0 step 600 python -u bench.py --inproc --gpus 8 --steps 5 --warmup 1 > $OUT/inproc.log 2>&1 || { tail -20 $OUT/inproc.log; exit 1; }
   BERT_DEVICES=0 step 600 python -u bench.py --inproc --gpus 1 --steps 5 --warmup 1 >> $OUT/inproc.log 2>&1 || { tail -20 $OUT/inproc.log; exit 1; }
 fi
+if has expab; then
+  # f16-expanded weights for compute-bound batches (default) against the fused
+  # dequantization at every batch size, alternating, same box
+  for r in 1 2; do
+    for e in 0 1; do
+      BERT_EXPAND_F16=$e step 200 python -u bench.py --no-cpu-baseline --no-probes --no-library --no-pmc > $OUT/expab_${e}_${r}.log 2>&1 || exit 1
+      python3 -c "import json,sys; d=json.loads(open('$OUT/expab_${e}_${r}.log').read().strip().splitlines()[-1]); print('expand=$e', d['value'], {k: round(v['avg_us'],1) for k,v in d['kernels'].items()})" | tee -a $OUT/expab.log
+    done
+  done
+fi
 if has gemmab; then
   # weight formats and tile configs of the C3 GEMM forms on random operands
   for f in 1 2; do SWEEP_FMT=$f step 120 python -u scripts/gemm_one.py all 0 20 >> $OUT/gemmab.log 2>&1 || exit 1; done
