@@ -235,7 +235,6 @@ Device::~Device()
     for (auto &p : pending_) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (auto e : free_events_) (void)hipEventDestroy(e);
     if (arena_) (void)hipFree(arena_);
-    if (arena16_) (void)hipFree(arena16_);
     if (ws_) (void)hipFree(ws_);
     if (h_ids_) (void)hipHostFree(h_ids_);
     if (h_cu_) (void)hipHostFree(h_cu_);
@@ -387,36 +386,6 @@ void Device::upload(const HostModel &m)
         D.b_o = (float *)P(x.bo); D.b_down = (float *)P(x.bdown);
         D.c1_qkv = (float *)P(x.c1q); D.c2_qkv = (float *)P(x.c2q); D.c1_up = (float *)P(x.c1u); D.c2_up = (float *)P(x.c2u);
         D.ln1_w = (float *)P(x.l1w); D.ln1_b = (float *)P(x.l1b); D.ln2_w = (float *)P(x.l2w); D.ln2_b = (float *)P(x.l2b);
-    }
-    // quantized files: the f16 expansion used by compute-bound batches (the
-    // K loop then spends no VALU on dequantization; same bits).  BERT_EXPAND_F16=0
-    // keeps the fused dequantization at every batch size.
-    static const bool expand_env = [] { const char *e = std::getenv("BERT_EXPAND_F16"); return !(e && *e == '0'); }();
-    if (expand_env && (wfmt_ == FMT_Q4_0 || wfmt_ == FMT_Q4_1 || wfmt_ == FMT_Q8_0)) {
-        size_t bytes = 0;
-        for (const DevLayer &D : layers_)
-            for (const DevWeight *w : {&D.qkv, &D.o, &D.up, &D.down}) bytes += align_up((size_t)w->N * w->K * 2, 256);
-        if (hipMalloc((void **)&arena16_, bytes) != hipSuccess) {
-            std::fprintf(stderr, "libbert: hipMalloc of %zu bytes (f16 weight copies) failed on device %d; "
-                                 "fused dequantization at every batch size\n", bytes, ordinal_);
-            (void)hipGetLastError();
-            arena16_ = nullptr;
-        } else {
-            size_t off = 0;
-            bool good = true;
-            for (DevLayer &D : layers_) {
-                const DevWeight *src[4] = {&D.qkv, &D.o, &D.up, &D.down};
-                DevWeight *dst[4] = {&D.qkv16, &D.o16, &D.up16, &D.down16};
-                for (int i = 0; i < 4; ++i) {
-                    good = good && launch_expand_f16(*src[i], arena16_ + off, stream_, *dst[i]) == 0;
-                    off += align_up((size_t)src[i]->N * src[i]->K * 2, 256);
-                }
-            }
-            if (!good || hipStreamSynchronize(stream_) != hipSuccess) {
-                std::fprintf(stderr, "libbert: weight expansion failed on device %d\n", ordinal_);
-                return;
-            }
-        }
     }
     ok_ = true;
 }
@@ -622,17 +591,13 @@ int Device::launch_all(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, in
     const int G = d / 32;
 
     const double att_flop = att_flop_;   // sum over sentences of 4 d len^2 (QK^T and PV), set by the caller
-    // compute-bound batches take the f16-expanded weights when the replica has them
-    const bool big = T >= GEMM_PAD_BIG && arena16_ != nullptr;
     for (int l = 0; l < hp_.n_layer; ++l) {
         const DevLayer &L = layers_[(size_t)l];
-        const DevWeight &Wqkv = big ? L.qkv16 : L.qkv, &Wo = big ? L.o16 : L.o;
-        const DevWeight &Wup = big ? L.up16 : L.up, &Wdown = big ? L.down16 : L.down;
         LnFold in;
         in.in_stats = st_;
         in.c1 = L.c1_qkv;
         begin(K_GEMM_QKV, s, ev);
-        launch_gemm(Wqkv, z_, M, L.c2_qkv, EPI_BIAS_F16, nullptr, qkv_, s, in);
+        launch_gemm(L.qkv, z_, M, L.c2_qkv, EPI_BIAS_F16, nullptr, qkv_, s, in);
         end(K_GEMM_QKV, s, ev, 2.0 * t * 3.0 * d * d);
         chk("gemm_qkv", l, qkv_, (size_t)T * 3 * d, 1);
 
@@ -646,7 +611,7 @@ int Device::launch_all(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, in
         r1.res_stats = st_; r1.res_g = gz; r1.res_b = bz;
         r1.g_next = L.ln1_w; r1.part = part_; r1.part_stride = (int32_t)rows_;
         begin(K_GEMM_O, s, ev);
-        launch_gemm(Wo, att_, M, L.b_o, EPI_BIAS_RES, z_, z_, s, r1);
+        launch_gemm(L.o, att_, M, L.b_o, EPI_BIAS_RES, z_, z_, s, r1);
         end(K_GEMM_O, s, ev, 2.0 * t * d * d);
         chk("gemm_o", l, z_, (size_t)T * d, 1);
 
@@ -657,7 +622,7 @@ int Device::launch_all(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, in
 
         in.c1 = L.c1_up;
         begin(K_GEMM_FFN_UP, s, ev);
-        launch_gemm(Wup, z_, M, L.c2_up, EPI_BIAS_GELU_F16, nullptr, ffn_, s, in);
+        launch_gemm(L.up, z_, M, L.c2_up, EPI_BIAS_GELU_F16, nullptr, ffn_, s, in);
         end(K_GEMM_FFN_UP, s, ev, 2.0 * t * d * f);
         chk("gemm_up", l, ffn_, (size_t)T * f, 1);
 
@@ -665,7 +630,7 @@ int Device::launch_all(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, in
         r2.res_stats = st_; r2.res_g = gz; r2.res_b = bz;
         r2.g_next = L.ln2_w; r2.part = part_; r2.part_stride = (int32_t)rows_;
         begin(K_GEMM_FFN_DOWN, s, ev);
-        launch_gemm(Wdown, ffn_, M, L.b_down, EPI_BIAS_RES, z_, z_, s, r2);
+        launch_gemm(L.down, ffn_, M, L.b_down, EPI_BIAS_RES, z_, z_, s, r2);
         end(K_GEMM_FFN_DOWN, s, ev, 2.0 * t * d * f);
         chk("gemm_down", l, z_, (size_t)T * d, 1);
 

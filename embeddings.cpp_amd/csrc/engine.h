@@ -29,9 +29,6 @@ struct KStats {
 
 struct DevLayer {
     DevWeight qkv, o, up, down;
-    // compute-bound batches (>= GEMM_PAD_BIG tokens): the same weights expanded
-    // once to f16 (launch_expand_f16; bitwise the fused dequantization), fmt 0 = none
-    DevWeight qkv16, o16, up16, down16;
     float *b_o = nullptr, *b_down = nullptr;
     // LN fold (kernels.h) of the projections that read a LayerNorm'd stream:
     // c1 = W gamma, c2 = b + W beta of the LN in front (QKV: the previous layer's
@@ -146,7 +143,6 @@ private:
 
     // weights
     char *arena_ = nullptr;
-    char *arena16_ = nullptr;       // expanded f16 copies of quantized linear weights
     size_t arena_size_ = 0, arena_used_ = 0;
     DevTable word_, type_, pos_;
     float *ln_e_w_ = nullptr, *ln_e_b_ = nullptr;

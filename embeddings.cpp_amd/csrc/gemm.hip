@@ -208,14 +208,17 @@ static_assert(z_waits<4, 4, 2, 4>().front == 3 * 6 && z_waits<4, 4, 2, 4>().back
 // The tile body: workgroup b of a grid of nTiles tiles (nN column tiles),
 // staging X in `smem` (NS * BM * 128 B of LDS) and the epilogue operands
 // behind it (zepi_lds).
-template <int FMT, int EPI, bool LNF, int NW, int BM, int NS, int FA, int WR>
+template <int FMT, int EPI, bool LNF, int NW, int BM, int NS, int FA, int WR, int NT>
 __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b, DevWeight W,
                                            const h16 *__restrict__ X, const float *__restrict__ bias,
                                            const void *__restrict__ res, void *__restrict__ out, int nN, int nTiles,
                                            const LnFold &ln)
 {
-    constexpr int BN = 32 * NW * FA;
-    constexpr int NJ = BM / 16;                 // 16-token B fragments per k-slice
+    // NT waves along the tokens (each BM / NT of them), NW / NT along the features
+    static_assert(NW % NT == 0 && (BM / NT) % 32 == 0, "wave grid");
+    constexpr int NF = NW / NT;
+    constexpr int BN = 32 * NF * FA;
+    constexpr int NJ = BM / NT / 16;            // 16-token B fragments per k-slice (this wave's tokens)
     constexpr int PF = FA == 1 ? (NJ <= 4 ? 2 * NJ - 1 : 4) : 3;   // B-fragment read-ahead (items of 2 FA MFMAs)
     constexpr int XB = BM * ZK * 2;             // bytes per X stage
     constexpr int XG = XB / (64 * NW * 16);     // LDS-DMA instructions per wave per stage
@@ -238,7 +241,8 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     const int K = W.K, N = W.N, KS = K / ZK;
     const int KX = W.kx ? W.kx : K, KSX = KX / ZK;   // X columns (f32 hi/lo weights: K = 2 KX)
     const int fr = lane & 15, g = lane >> 4;
-    const int nw = n0 + 32 * FA * wave;         // this wave's first feature
+    const int mt = (BM / NT) * (wave / NF);     // this wave's first token row in the tile
+    const int nw = n0 + 32 * FA * (wave % NF);  // this wave's first feature
     const int grp = min(nw, N - 32) >> 5;       // its first 32-feature weight group (clamped past N)
     // the wave's further groups (clamped past N; wave-uniform byte / element offsets)
     int gq[FA], gd[FA];
@@ -335,8 +339,8 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     lds_barrier();
     ZSTAMP(1, __builtin_amdgcn_s_memtime());
 
-    const int sw = (fr >> 1) & 7;
-    const int rbase = fr << 7;
+    const int sw = (fr >> 1) & 7;               // mt is a multiple of 32: the row swizzle is fr's
+    const int rbase = (mt + fr) << 7;
     int st = 0;
 #ifdef GEMM_STAMPS
     // K-loop split (diagnostic): cycles in the load wait in front of each K-step's
@@ -468,7 +472,7 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
         constexpr int NP = NJ / 2, PW = NP < 4 ? NP : 4;
         uint4 rr[PW][2];
         auto ldres = [&](int jp) {
-            const int tok = m0 + 16 * (2 * jp + (g & 1)) + fr;
+            const int tok = m0 + mt + 16 * (2 * jp + (g & 1)) + fr;
 #pragma unroll
             for (int a = 0; a < 2; ++a)
                 rr[jp % PW][a] = *(const uint4 *)((const h16 *)res + (size_t)tok * N + cb + 16 * a);
@@ -481,7 +485,7 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
         for (int jp = 0; jp < NP; ++jp) {
             {
                 const int j = 2 * jp;
-                const int tok = m0 + 16 * (j + (g & 1)) + fr;
+                const int tok = m0 + mt + 16 * (j + (g & 1)) + fr;
                 const float2 stt = use_st ? estat[tok - m0] : float2{0.f, 1.f};
                 uint4 rcur[2] = {};
                 if constexpr (RES) {
@@ -565,29 +569,29 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     }
 }
 
-template <int FMT, int EPI, bool LNF, int NW, int BM, int NS, int FA, int WR>
+template <int FMT, int EPI, bool LNF, int NW, int BM, int NS, int FA, int WR, int NT>
 __global__ __launch_bounds__(64 * NW, 2) void gemmz_kernel(DevWeight W, const h16 *__restrict__ X,
                                                                const float *__restrict__ bias,
                                                                const void *__restrict__ res, void *__restrict__ out,
                                                                int nN, int nTiles, LnFold ln)
 {
-    __shared__ __attribute__((aligned(16))) char smem[NS * BM * ZK * 2 + zepi_lds<EPI, LNF, 32 * NW * FA, BM>()];
+    __shared__ __attribute__((aligned(16))) char smem[NS * BM * ZK * 2 + zepi_lds<EPI, LNF, 32 * (NW / NT) * FA, BM>()];
     // a grid smaller than nTiles walks the tiles b, b + grid, ... (persistent;
     // the host only launches it so when every wave of every tile has features,
     // so no wave leaves the body early and the barrier between tiles is reached
     // by all)
     for (int b = blockIdx.x; b < nTiles; b += gridDim.x) {
-        gemmz_body<FMT, EPI, LNF, NW, BM, NS, FA, WR>(smem, b, W, X, bias, res, out, nN, nTiles, ln);
+        gemmz_body<FMT, EPI, LNF, NW, BM, NS, FA, WR, NT>(smem, b, W, X, bias, res, out, nN, nTiles, ln);
         ZSTAMP(3, __builtin_amdgcn_s_memtime());
         if (b + (int)gridDim.x < nTiles) lds_barrier();   // LDS (X ring, epilogue operands) reused
     }
 }
 
-template <int FMT, int NW, int BM, int NS, int FA = 1, int WR = 3>
+template <int FMT, int NW, int BM, int NS, int FA = 1, int WR = 3, int NT = 1>
 void dispatch_z(const DevWeight &W, const h16 *x, int M, const float *bias, int epi, const void *res, void *out,
                 hipStream_t s, const LnFold &ln, bool lnf)
 {
-    constexpr int BN = 32 * NW * FA;
+    constexpr int BN = 32 * (NW / NT) * FA;
     const int nN = (W.N + BN - 1) / BN, nTiles = (M / BM) * nN;
     // Persistent when a launch is at most two rounds of two workgroups per CU
     // (the N = d GEMMs at C3: 768 tiles = 1.5 rounds): 2 workgroups per CU walk
@@ -602,14 +606,14 @@ void dispatch_z(const DevWeight &W, const h16 *x, int M, const float *bias, int 
     if (persist > 0 && W.N % BN == 0) grid = std::min(nTiles, persist * cus);
     auto go = [&](auto kern) { kern<<<grid, 64 * NW, 0, s>>>(W, x, bias, res, out, nN, nTiles, ln); };
     if (epi == EPI_BIAS_F16) {
-        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_F16, true, NW, BM, NS, FA, WR>);
-        else go(gemmz_kernel<FMT, EPI_BIAS_F16, false, NW, BM, NS, FA, WR>);
+        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_F16, true, NW, BM, NS, FA, WR, NT>);
+        else go(gemmz_kernel<FMT, EPI_BIAS_F16, false, NW, BM, NS, FA, WR, NT>);
     } else if (epi == EPI_BIAS_GELU_F16) {
-        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_GELU_F16, true, NW, BM, NS, FA, WR>);
-        else go(gemmz_kernel<FMT, EPI_BIAS_GELU_F16, false, NW, BM, NS, FA, WR>);
+        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_GELU_F16, true, NW, BM, NS, FA, WR, NT>);
+        else go(gemmz_kernel<FMT, EPI_BIAS_GELU_F16, false, NW, BM, NS, FA, WR, NT>);
     } else {
-        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_RES, true, NW, BM, NS, FA, WR>);
-        else go(gemmz_kernel<FMT, EPI_BIAS_RES, false, NW, BM, NS, FA, WR>);
+        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_RES, true, NW, BM, NS, FA, WR, NT>);
+        else go(gemmz_kernel<FMT, EPI_BIAS_RES, false, NW, BM, NS, FA, WR, NT>);
     }
 }
 
@@ -622,31 +626,19 @@ void launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, 
         // (measured fastest at C3 once there are two per CU, profiles/r01_gemm16_sweep.log),
         // else 128 x 128 once there is one per CU, else 64 x 64 (small batches)
         const long n128 = (W.N + 127) / 128, cus = device_cu_count();
-        cfg = (M % 256 == 0 && (M / 256) * n128 >= 2 * cus) ? 2 : (M % 128 == 0 && (M / 128) * n128 >= cus) ? 3 : 4;
+        // small batches: BERT_GEMM_SMALL picks the 64-row form (4: 64 x 64 on 2 waves,
+        // 7: 64 x 64 on 4 waves, 8: 64 x 32 on 2 waves; the same bits)
+        static const int small = [] { const char *e = std::getenv("BERT_GEMM_SMALL"); const int v = e ? std::atoi(e) : 4;
+                                      return (v == 7 || v == 8) ? v : 4; }();
+        cfg = (M % 256 == 0 && (M / 256) * n128 >= 2 * cus) ? 2 : (M % 128 == 0 && (M / 128) * n128 >= cus) ? 3 : small;
     }
     if (cfg == 2 && M % 256 == 0) dispatch_z<FMT, 4, 256, 2>(W, x, M, bias, epi, res, out, s, ln, lnf);
     else if (cfg == 5 && M % 128 == 0) dispatch_z<FMT, 4, 128, 4, 2>(W, x, M, bias, epi, res, out, s, ln, lnf);
     else if (cfg != 4 && M % 128 == 0) dispatch_z<FMT, 4, 128, 4>(W, x, M, bias, epi, res, out, s, ln, lnf);
     else if (cfg == 6 && M % 64 == 0) dispatch_z<FMT, 2, 64, 4, 1, 4>(W, x, M, bias, epi, res, out, s, ln, lnf);
+    else if (cfg == 7 && M % 64 == 0) dispatch_z<FMT, 4, 64, 4, 1, 3, 2>(W, x, M, bias, epi, res, out, s, ln, lnf);
+    else if (cfg == 8 && M % 64 == 0) dispatch_z<FMT, 2, 64, 4, 1, 3, 2>(W, x, M, bias, epi, res, out, s, ln, lnf);
     else dispatch_z<FMT, 2, 64, 4>(W, x, M, bias, epi, res, out, s, ln, lnf);
-}
-
-// Weight expansion to the f16 lane-order layout (kernels.h): each lane record's
-// four A fragments exactly as the GEMM's in-register dequantization produces
-// them (ZRegs<FMT>::frag), so a GEMM on the expanded copy gives the bits of the
-// fused one.  One thread per lane record.
-template <int FMT>
-__global__ __launch_bounds__(256) void expand_f16_kernel(DevWeight W, uint4 *__restrict__ dst, int n_rec)
-{
-    const int r = blockIdx.x * 256 + threadIdx.x;
-    if (r >= n_rec) return;
-    const int G = W.N / 32;
-    const int lane = r & 63, grp = (r >> 6) % G, ks = (r >> 6) / G, fr = lane & 15;
-    ZRegs<FMT> z;
-    z.load((const uint8_t *)W.qs + (size_t)r * ZRegs<FMT>::QB, W.d + (((size_t)ks * G + grp) * 16 + fr) * 4,
-           FMT == FMT_Q4_1 ? W.m + (((size_t)ks * G + grp) * 16 + fr) * 4 : nullptr);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) dst[(size_t)r * 4 + u] = __builtin_bit_cast(uint4, z.frag(u));
 }
 
 }  // namespace
@@ -678,24 +670,6 @@ extern "C" __attribute__((visibility("default"))) int bertx_gemm_stamps(unsigned
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gemm_stamps), n * 8) == hipSuccess ? 0 : -1;
 }
 #endif
-
-int launch_expand_f16(const DevWeight &W, void *dst, hipStream_t s, DevWeight &out)
-{
-    if (W.N % 32 || W.K % ZK || W.kx) return -1;
-    const int n_rec = (W.K / ZK) * (W.N / 32) * 64, grid = (n_rec + 255) / 256;
-    switch (W.fmt) {
-    case FMT_Q4_0: expand_f16_kernel<FMT_Q4_0><<<grid, 256, 0, s>>>(W, (uint4 *)dst, n_rec); break;
-    case FMT_Q4_1: expand_f16_kernel<FMT_Q4_1><<<grid, 256, 0, s>>>(W, (uint4 *)dst, n_rec); break;
-    case FMT_Q8_0: expand_f16_kernel<FMT_Q8_0><<<grid, 256, 0, s>>>(W, (uint4 *)dst, n_rec); break;
-    default: return -1;
-    }
-    out = DevWeight();
-    out.fmt = FMT_F16;
-    out.N = W.N;
-    out.K = W.K;
-    out.qs = dst;
-    return 0;
-}
 
 int launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi, const void *res,
                 void *out, hipStream_t s, const LnFold &ln)

@@ -91,11 +91,6 @@ struct LnFold {
 // element-wise).  Returns 0, or -1 for an unsupported shape.
 int launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi,
                 const void *res, void *out, hipStream_t s, const LnFold &ln = LnFold());
-// The f16 lane-order copy of a quantized weight (q4_0 / q4_1 / q8_0): every A
-// fragment as the GEMM's in-register dequantization produces it, so a GEMM on
-// `out` (fmt f16, qs = dst, W.N * W.K * 2 bytes) gives the fused GEMM's bits.
-int launch_expand_f16(const DevWeight &W, void *dst, hipStream_t s, DevWeight &out);
-
 // Tests/benches: tile config (0 = heuristic, 2 = 4 waves 256x128, 3 = 4 waves 128x128,
 // 4 = 2 waves 64x64, 5 = 4 waves 128x256, 6 = 64x64 with the 4-set weight ring).
 // Per calling thread, so a test hook never changes a forward running on another thread.

@@ -30,13 +30,12 @@ if has inproc; then
   BERT_DEVICES=0,0,0,0,0,0,0,0 step 600 python -u bench.py --inproc --gpus 8 --steps 5 --warmup 1 > $OUT/inproc.log 2>&1 || { tail -20 $OUT/inproc.log; exit 1; }
   BERT_DEVICES=0 step 600 python -u bench.py --inproc --gpus 1 --steps 5 --warmup 1 >> $OUT/inproc.log 2>&1 || { tail -20 $OUT/inproc.log; exit 1; }
 fi
-if has expab; then
-  # f16-expanded weights for compute-bound batches (default) against the fused
-  # dequantization at every batch size, alternating, same box
+if has smallab; then
+  # the 64-row GEMM forms on the small-batch probes (C2, B 1 L 32), alternating
   for r in 1 2; do
-    for e in 0 1; do
-      BERT_EXPAND_F16=$e step 200 python -u bench.py --no-cpu-baseline --no-probes --no-library --no-pmc > $OUT/expab_${e}_${r}.log 2>&1 || exit 1
-      python3 -c "import json,sys; d=json.loads(open('$OUT/expab_${e}_${r}.log').read().strip().splitlines()[-1]); print('expand=$e', d['value'], {k: round(v['avg_us'],1) for k,v in d['kernels'].items()})" | tee -a $OUT/expab.log
+    for c in 4 7 8; do
+      BERT_GEMM_SMALL=$c step 300 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-library --no-pmc --no-profile > $OUT/smallab_${c}_${r}.log 2>&1 || exit 1
+      python3 -c "import json; d=json.loads(open('$OUT/smallab_${c}_${r}.log').read().strip().splitlines()[-1]); p=d['probes']; print('small=$c', 'C2', p['f16_mfma']['sentences_per_s'], 'B1', p['q4_0_hbm']['latency_us'], p['q4_0_hbm']['kernel_avg_us'])" | tee -a $OUT/smallab.log
     done
   done
 fi
