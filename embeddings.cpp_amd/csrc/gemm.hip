@@ -34,6 +34,7 @@
 #include <cstdlib>
 #include <utility>
 #include <atomic>
+#include <type_traits>
 
 namespace emb {
 
@@ -68,6 +69,22 @@ template <int N>
 __device__ __forceinline__ void zwait_lgkm(h16x8 &r)
 {
     asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(r) : "i"(N));
+}
+
+// A weight load of a K-loop tail step stands in as LQ dword LDS-DMA pieces into a
+// scratch slot: the same vmcnt events, no register written (the real loads'
+// data would be dead and hipcc deletes them; a dead asm load into a VGPR could
+// land after the register's reuse).  Issued from asm: invisible to hipcc's
+// waitcnt pass, like every counted X piece (their waits are the kernel's own).
+template <int N>
+__device__ __forceinline__ void ztail_dma(const void *g, uint32_t lds)
+{
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(g), "s"(lds) : "memory", "m0");
+#pragma clang diagnostic pop
 }
 
 // One K-step's worth of one lane's weight words for the wave's FA 32-feature
@@ -353,16 +370,23 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     // run-time no-op that stops hipcc's waitcnt pass from draining the ring with
     // vmcnt(0)); the K loop runs whole, unguarded WR-tuples so the count holds
     // on every path.
-    auto kstep = [&](ZSet<FMT, FA> &cur, ZSet<FMT, FA> &nxt, int ks) {
+    // A tail step (the remainder after the whole WR-tuples) loads no weights it
+    // will use: ztail_dma stands in for them, so the counts hold.
+    const uint32_t scratch = lds_u32(smem + NS * XB + zepi_lds<EPI, LNF, BN, BM>());
+    auto wload_or_tail = [&](ZSet<FMT, FA> &nxt, int kw, auto tail) {
+        if constexpr (decltype(tail)::value) ztail_dma<LQ>(wq + kw * qstep, scratch);
+        else wload(nxt, kw);
+    };
+    auto kstep = [&](ZSet<FMT, FA> &cur, ZSet<FMT, FA> &nxt, int ks, auto tail) {
         const int kx = min(ks + NS - 1, KS - 1), kw = min(ks + WR - 1, KS - 1);
         const int sx = st == 0 ? NS - 1 : st - 1;
         if constexpr (NS == 2) {
             issue_x(kx, sx);
             asm volatile("" ::: "memory");
-            wload(nxt, kw);
+            wload_or_tail(nxt, kw, tail);
             wait_vmcnt<ZW.front>();
         } else {
-            wload(nxt, kw);
+            wload_or_tail(nxt, kw, tail);
             asm volatile("" ::: "memory");
             issue_x(kx, sx);
 #ifdef GEMM_STAMPS
@@ -388,40 +412,36 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
         st = st == NS - 1 ? 0 : st + 1;
     };
     int ks = 0;
+    constexpr std::false_type body{};
+    constexpr std::true_type tail{};
     if constexpr (WR == 3) {
         for (; ks + 3 <= KS; ks += 3) {
-            kstep(w0, w2, ks);
-            kstep(w1, w0, ks + 1);
-            kstep(w2, w1, ks + 2);
+            kstep(w0, w2, ks, body);
+            kstep(w1, w0, ks + 1, body);
+            kstep(w2, w1, ks + 2, body);
         }
         if (ks < KS) {
-            kstep(w0, w2, ks);
-            if (ks + 1 < KS) kstep(w1, w0, ks + 1);
+            kstep(w0, w2, ks, tail);
+            if (ks + 1 < KS) kstep(w1, w0, ks + 1, tail);
         }
     } else {
         for (; ks + 4 <= KS; ks += 4) {
-            kstep(w0, w3, ks);
-            kstep(w1, w0, ks + 1);
-            kstep(w2, w1, ks + 2);
-            kstep(w3, w2, ks + 3);
+            kstep(w0, w3, ks, body);
+            kstep(w1, w0, ks + 1, body);
+            kstep(w2, w1, ks + 2, body);
+            kstep(w3, w2, ks + 3, body);
         }
         if (ks < KS) {
-            kstep(w0, w3, ks);
-            if (ks + 1 < KS) kstep(w1, w0, ks + 1);
-            if (ks + 2 < KS) kstep(w2, w1, ks + 2);
+            kstep(w0, w3, ks, tail);
+            if (ks + 1 < KS) kstep(w1, w0, ks + 1, tail);
+            if (ks + 2 < KS) kstep(w2, w1, ks + 2, tail);
         }
     }
-    // Every weight load the counts assume must be issued.  The tail steps' loads
-    // (clamped to the last K-step) feed no later step, so without a use hipcc
-    // deletes them as dead -- and a tail step's back wait, counted with those
-    // loads behind X(ks + 1), then leaves the last LQ pieces of X(ks + 1) in
-    // flight across the barrier (the NS 2 ring with KS % 3 == 2, the 4-set ring
-    // with KS % 4 == 2: the round-2 "4-set ring race").  An asm use of every set
-    // here keeps them live; it waits only for loads the epilogue would wait for.
-    w0.pin_all();
-    w1.pin_all();
-    w2.pin_all();
-    if constexpr (WR == 4) w3.pin_all();
+    // (Round 2's "4-set ring race": the tail steps' real weight loads feed no later
+    // step, so hipcc deleted them as dead, and a tail step's back wait -- counted
+    // with them behind X(ks + 1) -- left the last LQ pieces of X(ks + 1) in flight
+    // across the barrier: the NS 2 ring at KS % 3 == 2, the 4-set ring at
+    // KS % 4 == 2.  The tail now issues ztail_dma pieces in their place.)
     wait_vmcnt<0>();
     ZSTAMP(2, __builtin_amdgcn_s_memtime());
 #ifdef GEMM_STAMPS
@@ -575,7 +595,8 @@ __global__ __launch_bounds__(64 * NW, 2) void gemmz_kernel(DevWeight W, const h1
                                                                const void *__restrict__ res, void *__restrict__ out,
                                                                int nN, int nTiles, LnFold ln)
 {
-    __shared__ __attribute__((aligned(16))) char smem[NS * BM * ZK * 2 + zepi_lds<EPI, LNF, 32 * (NW / NT) * FA, BM>()];
+    __shared__ __attribute__((aligned(16))) char smem[NS * BM * ZK * 2 + zepi_lds<EPI, LNF, 32 * (NW / NT) * FA, BM>() +
+                                                      256];   // + the tail steps' scratch slot (ztail_dma)
     // a grid smaller than nTiles walks the tiles b, b + grid, ... (persistent;
     // the host only launches it so when every wave of every tile has features,
     // so no wave leaves the body early and the barrier between tiles is reached
@@ -626,10 +647,14 @@ void launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, 
         // (measured fastest at C3 once there are two per CU, profiles/r01_gemm16_sweep.log),
         // else 128 x 128 once there is one per CU, else 64 x 64 (small batches)
         const long n128 = (W.N + 127) / 128, cus = device_cu_count();
-        // small batches: BERT_GEMM_SMALL picks the 64-row form (4: 64 x 64 on 2 waves,
-        // 7: 64 x 64 on 4 waves, 8: 64 x 32 on 2 waves; the same bits)
-        static const int small = [] { const char *e = std::getenv("BERT_GEMM_SMALL"); const int v = e ? std::atoi(e) : 4;
-                                      return (v == 7 || v == 8) ? v : 4; }();
+        // small batches: 64-row tiles; while they fill less than half the CUs, on 4
+        // waves (2 along the tokens: every SIMD of a CU works, each wave's K-step
+        // half as long; B = 1, L = 32: 632 -> 571 us), else on 2 (C2's O-proj and
+        // FFN-down: the 4-wave form 6 % slower there).  Same bits either way.
+        // BERT_GEMM_SMALL = 4 / 7 / 8 forces one form (8: 64 x 32 on 2 waves).
+        static const int small_env = [] { const char *e = std::getenv("BERT_GEMM_SMALL"); return e ? std::atoi(e) : 0; }();
+        const long n64 = (long)(M / 64) * ((W.N + 63) / 64);
+        const int small = (small_env == 4 || small_env == 7 || small_env == 8) ? small_env : (2 * n64 < cus ? 7 : 4);
         cfg = (M % 256 == 0 && (M / 256) * n128 >= 2 * cus) ? 2 : (M % 128 == 0 && (M / 128) * n128 >= cus) ? 3 : small;
     }
     if (cfg == 2 && M % 256 == 0) dispatch_z<FMT, 4, 256, 2>(W, x, M, bias, epi, res, out, s, ln, lnf);
