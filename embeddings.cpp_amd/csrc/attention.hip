@@ -3,6 +3,7 @@
 #include "kernels.h"
 
 #include <cmath>
+#include <cstdlib>
 
 namespace emb {
 
@@ -390,6 +391,7 @@ extern "C" __attribute__((visibility("default"))) int bertx_att_stamps(unsigned 
 #define ASTAMP(k, v) do { } while (0)
 #endif
 
+template <bool LATE_STORE>
 __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restrict__ qkv,
                                                               const int32_t *__restrict__ cu, int d, int nh,
                                                               int n_items, float sl2, h16 *__restrict__ out)
@@ -643,23 +645,22 @@ __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restr
             }
         }
         ASTAMP(4, __builtin_amdgcn_s_memtime());
-        // the next item's Q (the 4 youngest loads; none <=> no region-A pieces
-        // either), then every older piece: the next item's region A
-        if (more) {
-            load_q(nx);
-            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        } else {
-            wait_all_vm();
-        }
-        __syncthreads();                                  // S: region B is free
-        ASTAMP(5, __builtin_amdgcn_s_memtime());
-        if (active) {
+        // The item's rows are stored BEFORE the S barrier, so a wave that finishes
+        // early writes while the slower ones still compute (after S, all 16 waves
+        // stored at once: ~3k cycles of write back-pressure per item).  The stores
+        // are bounds-checked buffer stores on every lane of an active wave (rows
+        // past the sentence fall outside the resource and are dropped), so an
+        // active wave issues exactly ATT_NST of them and the wait in front of S
+        // is exact: the next item's Q (4 loads) and the stores stay in flight,
+        // every older piece (the next item's region A) is retired.
+        if (more) load_q(nx);
+        auto store_rows = [&]() {
             // lane (q, hi) holds dh 8m + 4 hi .. +3 of chunks m = 4t + g; one
             // v_permlane32_swap per dword of the chunk pair (2p, 2p + 1) gives lane
             // (q, 0) dh 16p .. 16p + 7 and lane (q, 1) dh 16p + 8 .. 16p + 15: four
             // 16-B stores per lane instead of eight 8-B ones (the store tail is
             // issue-bound; cdna_hip_programming.md T21).  Both lanes of a pair
-            // hold the same query, so the swaps run before the q < len test.
+            // hold the same query, so the swaps run on every lane.
             const float inv = 1.0f / halves_sum(l);
             const int q = 32 * w + lq;
             uint32_t pk[DH / 8][2];
@@ -679,13 +680,30 @@ __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restr
                     pk[2 * p][k] = r[0];
                     pk[2 * p + 1][k] = r[1];
                 }
-            if (q < len) {
-                h16 *orow = out + (size_t)(cur.start + q) * d + cur.h * DH + 8 * hi;
+            // the item's rows [start, start + len) of `out` as the resource: a row
+            // q >= len lies past num_records and its store is dropped
+            const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+                (void *)(out + (size_t)cur.start * d), (short)0, cur.len * d * 2, 0x00020000);
+            const int ob = (q * d + cur.h * DH + 8 * hi) * 2;
 #pragma unroll
-                for (int p = 0; p < DH / 16; ++p)
-                    *(uint4 *)(orow + 16 * p) = uint4{pk[2 * p][0], pk[2 * p][1], pk[2 * p + 1][0], pk[2 * p + 1][1]};
+            for (int p = 0; p < DH / 16; ++p) {
+                typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+                const u32x4v v = {pk[2 * p][0], pk[2 * p][1], pk[2 * p + 1][0], pk[2 * p + 1][1]};
+                __builtin_amdgcn_raw_buffer_store_b128(v, ors, ob + 32 * p, 0, 0);
             }
+        };
+        static_assert(DH / 16 == 4, "four stores per active wave");
+        if (!LATE_STORE && active) {
+            store_rows();
+            if (more) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // 4 Q loads + 4 stores younger
+            else wait_all_vm();
+        } else {
+            if (more) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // the 4 Q loads younger
+            else wait_all_vm();
         }
+        ASTAMP(5, __builtin_amdgcn_s_memtime());
+        __syncthreads();                                  // S: region B is free
+        if (LATE_STORE && active) store_rows();           // (round 2's order: all waves store after S)
         ASTAMP(6, __builtin_amdgcn_s_memtime());
 #ifdef ATT_STAMPS
         ASTAMP(7, (unsigned long long)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11)));
@@ -712,8 +730,14 @@ void launch_attention(const uint16_t *qkv, const int32_t *cu, int32_t n_seqs, in
             const int n_items = n_seqs * n_head;
             const int cap = g_att_variant == 7 ? 7 : device_cu_count();
             const int grid = n_items < cap ? n_items : cap;
-            if (grid > 0)
-                attention_lds3_kernel<<<grid, 1024, 0, s>>>((const h16 *)qkv, cu, d, n_head, n_items, sl2, (h16 *)out);
+            // BERT_ATT_LATE_STORE=1: round 2's store order (after the S barrier), A/B
+            static const bool late = [] { const char *e = std::getenv("BERT_ATT_LATE_STORE"); return e && *e == '1'; }();
+            if (grid > 0) {
+                if (late)
+                    attention_lds3_kernel<true><<<grid, 1024, 0, s>>>((const h16 *)qkv, cu, d, n_head, n_items, sl2, (h16 *)out);
+                else
+                    attention_lds3_kernel<false><<<grid, 1024, 0, s>>>((const h16 *)qkv, cu, d, n_head, n_items, sl2, (h16 *)out);
+            }
         } else {
             attention_lds_kernel<32><<<g, blk, 0, s>>>((const h16 *)qkv, cu, d, n_head, sl2, (h16 *)out);
         }
