@@ -645,9 +645,10 @@ __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restr
             }
         }
         ASTAMP(4, __builtin_amdgcn_s_memtime());
-        // The item's rows are stored BEFORE the S barrier, so a wave that finishes
-        // early writes while the slower ones still compute (after S, all 16 waves
-        // stored at once: ~3k cycles of write back-pressure per item).  The stores
+        // LATE_STORE (production): the item's rows are stored after the S barrier.
+        // !LATE_STORE stores them BEFORE S, so a wave that finishes early writes
+        // while the slower ones still compute; measured 2 us slower (the early
+        // stores queue behind / in front of the next item's region-A pieces).  The stores
         // are bounds-checked buffer stores on every lane of an active wave (rows
         // past the sentence fall outside the resource and are dropped), so an
         // active wave issues exactly ATT_NST of them and the wait in front of S
@@ -703,7 +704,7 @@ __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restr
         }
         ASTAMP(5, __builtin_amdgcn_s_memtime());
         __syncthreads();                                  // S: region B is free
-        if (LATE_STORE && active) store_rows();           // (round 2's order: all waves store after S)
+        if (LATE_STORE && active) store_rows();           // production: all waves store after S
         ASTAMP(6, __builtin_amdgcn_s_memtime());
 #ifdef ATT_STAMPS
         ASTAMP(7, (unsigned long long)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11)));
@@ -730,8 +731,11 @@ void launch_attention(const uint16_t *qkv, const int32_t *cu, int32_t n_seqs, in
             const int n_items = n_seqs * n_head;
             const int cap = g_att_variant == 7 ? 7 : device_cu_count();
             const int grid = n_items < cap ? n_items : cap;
-            // BERT_ATT_LATE_STORE=1: round 2's store order (after the S barrier), A/B
-            static const bool late = [] { const char *e = std::getenv("BERT_ATT_LATE_STORE"); return e && *e == '1'; }();
+            // stores after the S barrier (default); BERT_ATT_EARLY_STORE=1 stores
+            // before it -- measured 2 us slower at C3 (70.3 vs 72.6 us,
+            // profiles/r03_attention_store_ab.log): the early stores compete with
+            // the next item's region-A loads the waves are still waiting for
+            static const bool late = [] { const char *e = std::getenv("BERT_ATT_EARLY_STORE"); return !(e && *e == '1'); }();
             if (grid > 0) {
                 if (late)
                     attention_lds3_kernel<true><<<grid, 1024, 0, s>>>((const h16 *)qkv, cu, d, n_head, n_items, sl2, (h16 *)out);

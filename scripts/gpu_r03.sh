@@ -31,11 +31,11 @@ if has inproc; then
   BERT_DEVICES=0 step 600 python -u bench.py --inproc --gpus 1 --steps 5 --warmup 1 >> $OUT/inproc.log 2>&1 || { tail -20 $OUT/inproc.log; exit 1; }
 fi
 if has attab; then
-  # attention store order: before the S barrier (default) vs after it (round 2)
+  # attention store order: after the S barrier (default) vs before it
   for r in 1 2; do
     for e in 0 1; do
-      BERT_ATT_LATE_STORE=$e step 200 python -u bench.py --no-cpu-baseline --no-probes --no-library --no-pmc > $OUT/attab_${e}_${r}.log 2>&1 || exit 1
-      python3 -c "import json; d=json.loads(open('$OUT/attab_${e}_${r}.log').read().strip().splitlines()[-1]); print('late_store=$e', d['value'], {k: round(v['avg_us'],1) for k,v in d['kernels'].items()})" | tee -a $OUT/attab.log
+      BERT_ATT_EARLY_STORE=$e step 200 python -u bench.py --no-cpu-baseline --no-probes --no-library --no-pmc > $OUT/attab_${e}_${r}.log 2>&1 || exit 1
+      python3 -c "import json; d=json.loads(open('$OUT/attab_${e}_${r}.log').read().strip().splitlines()[-1]); print('early_store=$e', d['value'], {k: round(v['avg_us'],1) for k,v in d['kernels'].items()})" | tee -a $OUT/attab.log
     done
   done
 fi
