@@ -103,9 +103,9 @@ struct ZSet {
 // ahead of their 2 FA MFMAs (a ring of PF + 1 fragments); A fragments
 // dequantized from the register set `cur` (s = 0 first half, s = 1 second);
 // acc[2 f + a] = features +32 f + 16 a.
-template <int NJ, int FA, int PF, class R, int... I>
+template <int NJ, int FA, int PF, class R, class H, int... I>
 __device__ __forceinline__ void zmma_items(const R &cur, uint32_t b0, uint32_t b1, f32x4 (&acc)[2 * FA][NJ],
-                                           std::integer_sequence<int, I...>)
+                                           const H &hook, std::integer_sequence<int, I...>)
 {
     constexpr int NI = 2 * NJ;
     h16x8 bq[PF + 1];
@@ -123,6 +123,7 @@ __device__ __forceinline__ void zmma_items(const R &cur, uint32_t b0, uint32_t b
     for (int f = 0; f < FA; ++f) { af[2 * f] = cur.r[f].frag(0); af[2 * f + 1] = cur.r[f].frag(2); }
     auto item = [&](auto ic) {
         constexpr int i = decltype(ic)::value;
+        hook(ic);                                     // (XI: an X piece of the next stage)
         rd(std::integral_constant<int, i + PF>{});
         constexpr int last = (i + PF < NI ? i + PF : NI - 1);
         zwait_lgkm<last - i>(bq[i % (PF + 1)]);
@@ -173,7 +174,7 @@ constexpr int zepi_lds()
 // state leaves those W(ks) unretired ("the 4-set ring race").
 struct ZWaits { int prologue, front, back; };
 
-template <int NS, int WR, int LQ, int XG>
+template <int NS, int WR, int LQ, int XG, int XI = 0>
 constexpr ZWaits z_waits()
 {
     constexpr int S = 16;                        // steps replayed (periodic long before)
@@ -196,9 +197,17 @@ constexpr ZWaits z_waits()
     for (int j = 2; j < WR - 1; ++j) add(0, j);
     ZWaits w{mn(after(0, 0), after(1, 0)), 1 << 20, 1 << 20};
     for (int ks = 0; ks < S; ++ks) {
-        if (NS == 2) { add(1, ks + 1); add(0, ks + WR - 1); }
-        else { add(0, ks + WR - 1); add(1, ks + NS - 1); }
-        w.front = mn(w.front, after(0, ks));
+        if (XI) {
+            // interleaved X: W(ks + WR - 1), the front wait, then X(ks + NS - 1)'s
+            // pieces among the step's MFMAs, the back wait
+            add(0, ks + WR - 1);
+            w.front = mn(w.front, after(0, ks));
+            add(1, ks + NS - 1);
+        } else {
+            if (NS == 2) { add(1, ks + 1); add(0, ks + WR - 1); }
+            else { add(0, ks + WR - 1); add(1, ks + NS - 1); }
+            w.front = mn(w.front, after(0, ks));
+        }
         w.back = mn(w.back, mn(after(1, ks + 1), after(0, ks + 1)));
     }
     return w;
@@ -216,6 +225,13 @@ static_assert(z_waits<4, 3, 4, 4>().front == 2 * 8 + 4 && z_waits<4, 3, 4, 4>().
 static_assert(z_waits<2, 3, 2, 8>().front == 2 * (2 + 8) && z_waits<2, 3, 2, 8>().back == 2 &&
                   z_waits<2, 3, 2, 8>().prologue == 2,
               "derived waits, 256x128 q4_0");
+// interleaved X pieces (NS 2): the front wait sees W(ks + 1), X(ks), W(ks + 2)
+// behind W(ks); the back wait retires everything (X(ks + 1) was issued last)
+static_assert(z_waits<2, 3, 2, 8, 1>().front == 8 + 2 * 2 && z_waits<2, 3, 2, 8, 1>().back == 0 &&
+                  z_waits<2, 3, 2, 8, 1>().prologue == 2,
+              "derived waits, 256x128 q4_0, interleaved X");
+static_assert(z_waits<4, 3, 2, 4, 2>().front == 2 * 2 + 2 * 4 && z_waits<4, 3, 2, 4, 2>().back == 2 + 2 * 4,
+              "derived waits, 128x128 / 64x64 q4_0, interleaved X");
 // the 4-set ring: the steady state has 3P + XG behind W(ks) (q4_0: 22) but the
 // two steps after the prologue only 3P (18)
 static_assert(z_waits<4, 4, 2, 4>().front == 3 * 6 && z_waits<4, 4, 2, 4>().back == 2 * 6 &&
@@ -225,7 +241,7 @@ static_assert(z_waits<4, 4, 2, 4>().front == 3 * 6 && z_waits<4, 4, 2, 4>().back
 // The tile body: workgroup b of a grid of nTiles tiles (nN column tiles),
 // staging X in `smem` (NS * BM * 128 B of LDS) and the epilogue operands
 // behind it (zepi_lds).
-template <int FMT, int EPI, bool LNF, int NW, int BM, int NS, int FA, int WR, int NT>
+template <int FMT, int EPI, bool LNF, int NW, int BM, int NS, int FA, int WR, int NT, int XI>
 __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b, DevWeight W,
                                            const h16 *__restrict__ X, const float *__restrict__ bias,
                                            const void *__restrict__ res, void *__restrict__ out, int nN, int nTiles,
@@ -244,7 +260,7 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     constexpr int P = LQ + XG;                  // vector-memory ops issued per K-step per wave
     static_assert(NS >= 2 && NS <= 4 && XG >= 2 && XG % 2 == 0, "X ring");
     static_assert(WR == 3 || WR == 4, "weight register ring: 3 or 4 sets");
-    constexpr ZWaits ZW = z_waits<NS, WR, LQ, XG>();
+    constexpr ZWaits ZW = z_waits<NS, WR, LQ, XG, XI>();
     static_assert(ZW.prologue >= 0 && ZW.front >= 0 && ZW.back >= 0 && ZW.front < 64 && P <= 63,
                   "vmcnt range (6 bits)");
     (void)P;
@@ -282,13 +298,15 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
         const int r = 8 * XG * wave + 8 * i + (lane >> 3);
         xvo[i] = (uint32_t)(r * KX + (((lane & 7) ^ ((r >> 1) & 7)) * 8)) * 2u;
     }
-    auto issue_x = [&](int ks, int stage) {
+    auto issue_x_piece = [&](int ks, int stage, int i) {
         char *dst = smem + stage * XB + ((8 * XG * wave) << 7);
         const int kc = ks < KSX ? ks : ks - KSX;   // the X column block of K-step ks
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_void_t *)(dst + (i << 10)), 16, xvo[i & 1],
+                                                 ((i >> 1) * 16 * KX + kc * ZK) * 2, 0, 0);
+    };
+    auto issue_x = [&](int ks, int stage) {
 #pragma unroll
-        for (int i = 0; i < XG; ++i)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_void_t *)(dst + (i << 10)), 16, xvo[i & 1],
-                                                     ((i >> 1) * 16 * KX + kc * ZK) * 2, 0, 0);
+        for (int i = 0; i < XG; ++i) issue_x_piece(ks, stage, i);
     };
     const uint8_t *wq = (const uint8_t *)W.qs + ((size_t)grp * 64 + lane) * QB;
     const uint16_t *wd = W.d + ((size_t)grp * 16 + fr) * 4;
@@ -380,9 +398,19 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     auto kstep = [&](ZSet<FMT, FA> &cur, ZSet<FMT, FA> &nxt, int ks, auto tail) {
         const int kx = min(ks + NS - 1, KS - 1), kw = min(ks + WR - 1, KS - 1);
         const int sx = st == 0 ? NS - 1 : st - 1;
-        if constexpr (NS == 2) {
+        if constexpr (XI) {
+            wload_or_tail(nxt, kw, tail);
+            wait_vmcnt<ZW.front>();
+        } else if constexpr (NS == 2) {
+#ifdef GEMM_STAMPS
+            // (NS 2: slot 6 holds the cycles of the X pieces' issue instead of the front wait)
+            const unsigned long long zd = __builtin_amdgcn_s_memtime();
+#endif
             issue_x(kx, sx);
             asm volatile("" ::: "memory");
+#ifdef GEMM_STAMPS
+            zw_front += __builtin_amdgcn_s_memtime() - zd;
+#endif
             wload_or_tail(nxt, kw, tail);
             wait_vmcnt<ZW.front>();
         } else {
@@ -399,7 +427,15 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
         }
         cur.pin_all();
         const uint32_t xs = lds_u32(smem + st * XB + rbase);
-        zmma_items<NJ, FA, PF>(cur, xs + ((g ^ sw) << 4), xs + (((4 + g) ^ sw) << 4), acc,
+        // XI: X(ks + 1)'s XG pieces among the first XG * XS items (one every XS), so
+        // the CU's texture path takes a wave's pieces between its MFMAs instead of
+        // in one burst in front of them
+        constexpr int XS = XI == 1 && 2 * NJ / XG >= 2 ? 2 : 1;   // XI 2: one per item (measured best), 1: every second
+        auto hook = [&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            if constexpr (XI && i % XS == 0 && i / XS < XG) issue_x_piece(kx, sx, i / XS);
+        };
+        zmma_items<NJ, FA, PF>(cur, xs + ((g ^ sw) << 4), xs + (((4 + g) ^ sw) << 4), acc, hook,
                        std::make_integer_sequence<int, 2 * NJ>{});
 #ifdef GEMM_STAMPS
         const unsigned long long zb = __builtin_amdgcn_s_memtime();
@@ -589,7 +625,7 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     }
 }
 
-template <int FMT, int EPI, bool LNF, int NW, int BM, int NS, int FA, int WR, int NT>
+template <int FMT, int EPI, bool LNF, int NW, int BM, int NS, int FA, int WR, int NT, int XI>
 __global__ __launch_bounds__(64 * NW, 2) void gemmz_kernel(DevWeight W, const h16 *__restrict__ X,
                                                                const float *__restrict__ bias,
                                                                const void *__restrict__ res, void *__restrict__ out,
@@ -602,13 +638,13 @@ __global__ __launch_bounds__(64 * NW, 2) void gemmz_kernel(DevWeight W, const h1
     // so no wave leaves the body early and the barrier between tiles is reached
     // by all)
     for (int b = blockIdx.x; b < nTiles; b += gridDim.x) {
-        gemmz_body<FMT, EPI, LNF, NW, BM, NS, FA, WR, NT>(smem, b, W, X, bias, res, out, nN, nTiles, ln);
+        gemmz_body<FMT, EPI, LNF, NW, BM, NS, FA, WR, NT, XI>(smem, b, W, X, bias, res, out, nN, nTiles, ln);
         ZSTAMP(3, __builtin_amdgcn_s_memtime());
         if (b + (int)gridDim.x < nTiles) lds_barrier();   // LDS (X ring, epilogue operands) reused
     }
 }
 
-template <int FMT, int NW, int BM, int NS, int FA = 1, int WR = 3, int NT = 1>
+template <int FMT, int NW, int BM, int NS, int FA = 1, int WR = 3, int NT = 1, int XI = 0>
 void dispatch_z(const DevWeight &W, const h16 *x, int M, const float *bias, int epi, const void *res, void *out,
                 hipStream_t s, const LnFold &ln, bool lnf)
 {
@@ -627,14 +663,14 @@ void dispatch_z(const DevWeight &W, const h16 *x, int M, const float *bias, int 
     if (persist > 0 && W.N % BN == 0) grid = std::min(nTiles, persist * cus);
     auto go = [&](auto kern) { kern<<<grid, 64 * NW, 0, s>>>(W, x, bias, res, out, nN, nTiles, ln); };
     if (epi == EPI_BIAS_F16) {
-        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_F16, true, NW, BM, NS, FA, WR, NT>);
-        else go(gemmz_kernel<FMT, EPI_BIAS_F16, false, NW, BM, NS, FA, WR, NT>);
+        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_F16, true, NW, BM, NS, FA, WR, NT, XI>);
+        else go(gemmz_kernel<FMT, EPI_BIAS_F16, false, NW, BM, NS, FA, WR, NT, XI>);
     } else if (epi == EPI_BIAS_GELU_F16) {
-        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_GELU_F16, true, NW, BM, NS, FA, WR, NT>);
-        else go(gemmz_kernel<FMT, EPI_BIAS_GELU_F16, false, NW, BM, NS, FA, WR, NT>);
+        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_GELU_F16, true, NW, BM, NS, FA, WR, NT, XI>);
+        else go(gemmz_kernel<FMT, EPI_BIAS_GELU_F16, false, NW, BM, NS, FA, WR, NT, XI>);
     } else {
-        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_RES, true, NW, BM, NS, FA, WR, NT>);
-        else go(gemmz_kernel<FMT, EPI_BIAS_RES, false, NW, BM, NS, FA, WR, NT>);
+        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_RES, true, NW, BM, NS, FA, WR, NT, XI>);
+        else go(gemmz_kernel<FMT, EPI_BIAS_RES, false, NW, BM, NS, FA, WR, NT, XI>);
     }
 }
 
@@ -656,8 +692,19 @@ void launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, 
         const long n64 = (long)(M / 64) * ((W.N + 63) / 64);
         const int small = (small_env == 4 || small_env == 7 || small_env == 8) ? small_env : (2 * n64 < cus ? 7 : 4);
         cfg = (M % 256 == 0 && (M / 256) * n128 >= 2 * cus) ? 2 : (M % 128 == 0 && (M / 128) * n128 >= cus) ? 3 : small;
+        // BERT_GEMM_XI = 1: the 128- and 64-row forms with the X pieces among the
+        // MFMAs too (cfg 13 / 14 / 15; A/B)
+        static const bool xi_env = [] { const char *e = std::getenv("BERT_GEMM_XI"); return e && *e == '1'; }();
+        if (xi_env) cfg = cfg == 3 ? 13 : cfg == 4 ? 14 : cfg == 7 ? 15 : cfg;
     }
-    if (cfg == 2 && M % 256 == 0) dispatch_z<FMT, 4, 256, 2>(W, x, M, bias, epi, res, out, s, ln, lnf);
+    // 256 x 128: the X pieces among the MFMAs (one per B-fragment item from the
+    // K-step's start; +1.2-1.6 % on the C3 forward over one burst in front of them,
+    // profiles/r03_gemm_xi_ab.log); cfg 11 keeps the burst form for A/B
+    if (cfg == 2 && M % 256 == 0) dispatch_z<FMT, 4, 256, 2, 1, 3, 1, 2>(W, x, M, bias, epi, res, out, s, ln, lnf);
+    else if (cfg == 11 && M % 256 == 0) dispatch_z<FMT, 4, 256, 2>(W, x, M, bias, epi, res, out, s, ln, lnf);
+    else if (cfg == 13 && M % 128 == 0) dispatch_z<FMT, 4, 128, 4, 1, 3, 1, 2>(W, x, M, bias, epi, res, out, s, ln, lnf);
+    else if (cfg == 14 && M % 64 == 0) dispatch_z<FMT, 2, 64, 4, 1, 3, 1, 2>(W, x, M, bias, epi, res, out, s, ln, lnf);
+    else if (cfg == 15 && M % 64 == 0) dispatch_z<FMT, 4, 64, 4, 1, 3, 2, 2>(W, x, M, bias, epi, res, out, s, ln, lnf);
     else if (cfg == 5 && M % 128 == 0) dispatch_z<FMT, 4, 128, 4, 2>(W, x, M, bias, epi, res, out, s, ln, lnf);
     else if (cfg != 4 && M % 128 == 0) dispatch_z<FMT, 4, 128, 4>(W, x, M, bias, epi, res, out, s, ln, lnf);
     else if (cfg == 6 && M % 64 == 0) dispatch_z<FMT, 2, 64, 4, 1, 4>(W, x, M, bias, epi, res, out, s, ln, lnf);

@@ -23,7 +23,7 @@ buf = (ctypes.c_ulonglong * n)()
 L.bertx_gemm_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
 assert L.bertx_gemm_stamps(buf, n) == 0
 a = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 8).astype(np.int64)
-nw = 4 if cfg in (2, 3, 5, 0) else 2
+nw = 8 if cfg in (9, 10) else 4 if cfg in (2, 3, 5, 0) else 2
 bm = {2: 256, 3: 128, 4: 64, 5: 128}.get(cfg, 256)
 bn = 256 if cfg == 5 else 32 * nw
 tiles = (M // bm) * ((N + bn - 1) // bn)

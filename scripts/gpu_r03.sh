@@ -54,6 +54,32 @@ if has gemmab; then
   SWEEP_FMT=2 step 120 python -u scripts/gemm_one.py all 5 20 >> $OUT/gemmab.log 2>&1 || exit 1
   cat $OUT/gemmab.log
 fi
+if has wide; then
+  # 8-wave 256 x 256 tiles (cfg 9 NS 2, cfg 10 NS 3; one workgroup per CU) against production (2)
+  for r in 1 2; do for c in 2 9 10; do step 120 python -u scripts/gemm_one.py all $c 20 >> $OUT/wide.log 2>&1 || exit 1; done; done
+  for c in 2 9 10; do STAMPS_LIB=build/stamps/libbert.so step 120 python -u scripts/gemm_stamps.py 3072 768 1 $c >> $OUT/wide_stamps.log 2>&1 || exit 1; done
+  cat $OUT/wide.log
+fi
+if has dmastamp; then
+  for a in "3072 768 1" "2304 768 0" "768 3072 2"; do STAMPS_LIB=build/stamps/libbert.so step 120 python -u scripts/gemm_stamps.py $a 2 >> $OUT/dma_stamps.log 2>&1 || exit 1; done
+  cat $OUT/dma_stamps.log
+fi
+if has xi; then
+  # X pieces interleaved among the MFMAs (cfg 11) against the burst in front of them (2)
+  for r in 1 2; do for c in 2 11 12; do step 120 python -u scripts/gemm_one.py all $c 20 >> $OUT/xi.log 2>&1 || exit 1; done; done
+  for r in 1 2; do for c in 0 11 12; do
+    BERT_GEMM_CFG=$c step 200 python -u bench.py --no-cpu-baseline --no-probes --no-library --no-pmc > $OUT/xi_${c}_${r}.log 2>&1 || exit 1
+    python3 -c "import json; d=json.loads(open('$OUT/xi_${c}_${r}.log').read().strip().splitlines()[-1]); print('cfg=$c', d['value'], {k: round(v['avg_us'],1) for k,v in d['kernels'].items()})" | tee -a $OUT/xi.log
+  done; done
+  cat $OUT/xi.log
+fi
+if has xismall; then
+  # interleaved X pieces on the 128- and 64-row forms (BERT_GEMM_XI=1) on the probes, alternating
+  for r in 1 2; do for e in 0 1; do
+    BERT_GEMM_XI=$e step 300 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-library --no-pmc --no-profile > $OUT/xismall_${e}_${r}.log 2>&1 || exit 1
+    python3 -c "import json; d=json.loads(open('$OUT/xismall_${e}_${r}.log').read().strip().splitlines()[-1]); p=d['probes']; print('xi=$e', 'C3', d['value'], 'C2', p['f16_mfma']['sentences_per_s'], 'B1', p['q4_0_hbm']['latency_us'])" | tee -a $OUT/xismall.log
+  done; done
+fi
 if has tok; then step 300 python -u scripts/host_throughput.py tok --texts 4000 > $OUT/tok.log 2>&1 || exit 1; fi
 if has server; then step 400 python -u scripts/host_throughput.py server > $OUT/server.log 2>&1 || { tail -20 $OUT/server.log; exit 1; }; fi
 echo session-ok
