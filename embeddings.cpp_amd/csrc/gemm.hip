@@ -253,14 +253,24 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     constexpr int BN = 32 * NF * FA;
     constexpr int NJ = BM / NT / 16;            // 16-token B fragments per k-slice (this wave's tokens)
     constexpr int PF = FA == 1 ? (NJ <= 4 ? 2 * NJ - 1 : 4) : 3;   // B-fragment read-ahead (items of 2 FA MFMAs)
-    constexpr int XB = BM * ZK * 2;             // bytes per X stage
-    constexpr int XG = XB / (64 * NW * 16);     // LDS-DMA instructions per wave per stage
+    // X modes (XI): 0 one burst of pieces in front of the K-step's MFMAs, 1 / 2 the
+    // pieces among them (every second / every B-fragment item); 3 / 4 as 0 / 2 into
+    // a wave-private ring: each wave stages its own BM / NT token rows (the NF waves
+    // that share them each load a copy), so no barrier couples the waves in the K
+    // loop -- a wave's own covering vmcnt orders its ds_reads behind its pieces
+    // (MI355X_MICROARCH.md, co-residence item 7)
+    constexpr bool PRIV = XI >= 3;
+    constexpr int XMODE = XI == 3 ? 0 : XI == 4 ? 2 : XI;
+    constexpr int XB = BM * ZK * 2;             // bytes per shared X stage
+    constexpr int XBW = (BM / NT) * ZK * 2;     // bytes per wave-private stage
+    constexpr int RING = PRIV ? NW * NS * XBW : NS * XB;
+    constexpr int XG = PRIV ? XBW / 1024 : XB / (64 * NW * 16);   // LDS-DMA instructions per wave per stage
     constexpr int LQ = ZRegs<FMT>::LOADS * FA;
     constexpr int QB = ZRegs<FMT>::QB;
     constexpr int P = LQ + XG;                  // vector-memory ops issued per K-step per wave
     static_assert(NS >= 2 && NS <= 4 && XG >= 2 && XG % 2 == 0, "X ring");
     static_assert(WR == 3 || WR == 4, "weight register ring: 3 or 4 sets");
-    constexpr ZWaits ZW = z_waits<NS, WR, LQ, XG, XI>();
+    constexpr ZWaits ZW = z_waits<NS, WR, LQ, XG, XMODE>();
     static_assert(ZW.prologue >= 0 && ZW.front >= 0 && ZW.back >= 0 && ZW.front < 64 && P <= 63,
                   "vmcnt range (6 bits)");
     (void)P;
@@ -295,11 +305,11 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     uint32_t xvo[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-        const int r = 8 * XG * wave + 8 * i + (lane >> 3);
+        const int r = (PRIV ? mt : 8 * XG * wave) + 8 * i + (lane >> 3);
         xvo[i] = (uint32_t)(r * KX + (((lane & 7) ^ ((r >> 1) & 7)) * 8)) * 2u;
     }
     auto issue_x_piece = [&](int ks, int stage, int i) {
-        char *dst = smem + stage * XB + ((8 * XG * wave) << 7);
+        char *dst = PRIV ? smem + (wave * NS + stage) * XBW : smem + stage * XB + ((8 * XG * wave) << 7);
         const int kc = ks < KSX ? ks : ks - KSX;   // the X column block of K-step ks
         __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_void_t *)(dst + (i << 10)), 16, xvo[i & 1],
                                                  ((i >> 1) * 16 * KX + kc * ZK) * 2, 0, 0);
@@ -325,8 +335,8 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     constexpr int NA = zepi_arrays<EPI, LNF>();
     constexpr int FP = zkib(NA * BN * 4);       // pieces of the per-feature arrays
     constexpr int SP = LNF ? zkib(BM * 8) : 0;  // pieces of the row statistics
-    float *const efeat = (float *)(smem + NS * XB);
-    float2 *const estat = (float2 *)(smem + NS * XB + FP * 1024);
+    float *const efeat = (float *)(smem + RING);
+    float2 *const estat = (float2 *)(smem + RING + FP * 1024);
     const float2 *stp = RES ? ln.res_stats : ln.in_stats;
     if (wave == 0) {
         const float *arr[4] = {bias, RES ? ln.res_g : ln.c1, ln.res_b, ln.g_next};
@@ -375,7 +385,7 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     ZSTAMP(1, __builtin_amdgcn_s_memtime());
 
     const int sw = (fr >> 1) & 7;               // mt is a multiple of 32: the row swizzle is fr's
-    const int rbase = (mt + fr) << 7;
+    const int rbase = PRIV ? fr << 7 : (mt + fr) << 7;
     int st = 0;
 #ifdef GEMM_STAMPS
     // K-loop split (diagnostic): cycles in the load wait in front of each K-step's
@@ -390,7 +400,7 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     // on every path.
     // A tail step (the remainder after the whole WR-tuples) loads no weights it
     // will use: ztail_dma stands in for them, so the counts hold.
-    const uint32_t scratch = lds_u32(smem + NS * XB + zepi_lds<EPI, LNF, BN, BM>());
+    const uint32_t scratch = lds_u32(smem + RING + zepi_lds<EPI, LNF, BN, BM>());
     auto wload_or_tail = [&](ZSet<FMT, FA> &nxt, int kw, auto tail) {
         if constexpr (decltype(tail)::value) ztail_dma<LQ>(wq + kw * qstep, scratch);
         else wload(nxt, kw);
@@ -398,10 +408,10 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     auto kstep = [&](ZSet<FMT, FA> &cur, ZSet<FMT, FA> &nxt, int ks, auto tail) {
         const int kx = min(ks + NS - 1, KS - 1), kw = min(ks + WR - 1, KS - 1);
         const int sx = st == 0 ? NS - 1 : st - 1;
-        if constexpr (XI) {
+        if constexpr (XMODE) {
             wload_or_tail(nxt, kw, tail);
             wait_vmcnt<ZW.front>();
-        } else if constexpr (NS == 2) {
+        } else if constexpr (NS == 2 && !PRIV) {
 #ifdef GEMM_STAMPS
             // (NS 2: slot 6 holds the cycles of the X pieces' issue instead of the front wait)
             const unsigned long long zd = __builtin_amdgcn_s_memtime();
@@ -426,14 +436,14 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
 #endif
         }
         cur.pin_all();
-        const uint32_t xs = lds_u32(smem + st * XB + rbase);
+        const uint32_t xs = lds_u32(smem + (PRIV ? (wave * NS + st) * XBW : st * XB) + rbase);
         // XI: X(ks + 1)'s XG pieces among the first XG * XS items (one every XS), so
         // the CU's texture path takes a wave's pieces between its MFMAs instead of
         // in one burst in front of them
-        constexpr int XS = XI == 1 && 2 * NJ / XG >= 2 ? 2 : 1;   // XI 2: one per item (measured best), 1: every second
+        constexpr int XS = XMODE == 1 && 2 * NJ / XG >= 2 ? 2 : 1;   // mode 2: one per item (measured best), 1: every second
         auto hook = [&](auto ic) {
             constexpr int i = decltype(ic)::value;
-            if constexpr (XI && i % XS == 0 && i / XS < XG) issue_x_piece(kx, sx, i / XS);
+            if constexpr (XMODE && i % XS == 0 && i / XS < XG) issue_x_piece(kx, sx, i / XS);
         };
         zmma_items<NJ, FA, PF>(cur, xs + ((g ^ sw) << 4), xs + (((4 + g) ^ sw) << 4), acc, hook,
                        std::make_integer_sequence<int, 2 * NJ>{});
@@ -441,7 +451,7 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
         const unsigned long long zb = __builtin_amdgcn_s_memtime();
 #endif
         wait_vmcnt<ZW.back>();
-        lds_barrier();
+        if constexpr (!PRIV) lds_barrier();
 #ifdef GEMM_STAMPS
         zw_back += __builtin_amdgcn_s_memtime() - zb;
 #endif
@@ -631,7 +641,7 @@ __global__ __launch_bounds__(64 * NW, 2) void gemmz_kernel(DevWeight W, const h1
                                                                const void *__restrict__ res, void *__restrict__ out,
                                                                int nN, int nTiles, LnFold ln)
 {
-    __shared__ __attribute__((aligned(16))) char smem[NS * BM * ZK * 2 + zepi_lds<EPI, LNF, 32 * (NW / NT) * FA, BM>() +
+    __shared__ __attribute__((aligned(16))) char smem[(XI >= 3 ? NW / NT : 1) * NS * BM * ZK * 2 + zepi_lds<EPI, LNF, 32 * (NW / NT) * FA, BM>() +
                                                       256];   // + the tail steps' scratch slot (ztail_dma)
     // a grid smaller than nTiles walks the tiles b, b + grid, ... (persistent;
     // the host only launches it so when every wave of every tile has features,
@@ -685,12 +695,14 @@ void launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, 
         const long n128 = (W.N + 127) / 128, cus = device_cu_count();
         // small batches: 64-row tiles; while they fill less than half the CUs, on 4
         // waves (2 along the tokens: every SIMD of a CU works, each wave's K-step
-        // half as long; B = 1, L = 32: 632 -> 571 us), else on 2 (C2's O-proj and
-        // FFN-down: the 4-wave form 6 % slower there).  Same bits either way.
-        // BERT_GEMM_SMALL = 4 / 7 / 8 forces one form (8: 64 x 32 on 2 waves).
+        // half as long; B = 1, L = 32: 632 -> 571 us) with wave-private X rings (no
+        // barrier in the K loop: 582 -> 567 us, profiles/r03_gemm_private_ab.log),
+        // else on 2 (C2's O-proj and FFN-down: the 4-wave forms 6-15 % slower
+        // there).  Same bits either way.  BERT_GEMM_SMALL = 4 / 7 / 8 / 16 / 17
+        // forces one form (8: 64 x 32 on 2 waves; 17: 4 with private rings).
         static const int small_env = [] { const char *e = std::getenv("BERT_GEMM_SMALL"); return e ? std::atoi(e) : 0; }();
         const long n64 = (long)(M / 64) * ((W.N + 63) / 64);
-        const int small = (small_env == 4 || small_env == 7 || small_env == 8) ? small_env : (2 * n64 < cus ? 7 : 4);
+        const int small = (small_env == 4 || small_env == 7 || small_env == 8 || small_env == 16 || small_env == 17) ? small_env : (2 * n64 < cus ? 16 : 4);
         cfg = (M % 256 == 0 && (M / 256) * n128 >= 2 * cus) ? 2 : (M % 128 == 0 && (M / 128) * n128 >= cus) ? 3 : small;
         // BERT_GEMM_XI = 1: the 128- and 64-row forms with the X pieces among the
         // MFMAs too (cfg 13 / 14 / 15; A/B)
@@ -705,6 +717,8 @@ void launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, 
     else if (cfg == 13 && M % 128 == 0) dispatch_z<FMT, 4, 128, 4, 1, 3, 1, 2>(W, x, M, bias, epi, res, out, s, ln, lnf);
     else if (cfg == 14 && M % 64 == 0) dispatch_z<FMT, 2, 64, 4, 1, 3, 1, 2>(W, x, M, bias, epi, res, out, s, ln, lnf);
     else if (cfg == 15 && M % 64 == 0) dispatch_z<FMT, 4, 64, 4, 1, 3, 2, 2>(W, x, M, bias, epi, res, out, s, ln, lnf);
+    else if (cfg == 16 && M % 64 == 0) dispatch_z<FMT, 4, 64, 4, 1, 3, 2, 3>(W, x, M, bias, epi, res, out, s, ln, lnf);
+    else if (cfg == 17 && M % 64 == 0) dispatch_z<FMT, 2, 64, 4, 1, 3, 1, 3>(W, x, M, bias, epi, res, out, s, ln, lnf);
     else if (cfg == 5 && M % 128 == 0) dispatch_z<FMT, 4, 128, 4, 2>(W, x, M, bias, epi, res, out, s, ln, lnf);
     else if (cfg != 4 && M % 128 == 0) dispatch_z<FMT, 4, 128, 4>(W, x, M, bias, epi, res, out, s, ln, lnf);
     else if (cfg == 6 && M % 64 == 0) dispatch_z<FMT, 2, 64, 4, 1, 4>(W, x, M, bias, epi, res, out, s, ln, lnf);

@@ -42,7 +42,7 @@ fi
 if has smallab; then
   # the 64-row GEMM forms on the small-batch probes (C2, B 1 L 32), alternating
   for r in 1 2; do
-    for c in 4 7 8; do
+    for c in ${SMALLC:-4 7 8}; do
       BERT_GEMM_SMALL=$c step 300 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-library --no-pmc --no-profile > $OUT/smallab_${c}_${r}.log 2>&1 || exit 1
       python3 -c "import json; d=json.loads(open('$OUT/smallab_${c}_${r}.log').read().strip().splitlines()[-1]); p=d['probes']; print('small=$c', 'C2', p['f16_mfma']['sentences_per_s'], 'B1', p['q4_0_hbm']['latency_us'], p['q4_0_hbm']['kernel_avg_us'])" | tee -a $OUT/smallab.log
     done

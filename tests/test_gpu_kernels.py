@@ -156,16 +156,17 @@ def test_f32_gemm_matches_numpy(lib, epi, N, K, M):
 
 
 @pytest.mark.parametrize("fmt", sorted(FMTS))
-@pytest.mark.parametrize("cfg", [2, 3, 4, 5, 6, 7, 8, 11, 13, 14, 15])
+@pytest.mark.parametrize("cfg", [2, 3, 4, 5, 6, 7, 8, 11, 13, 14, 15, 16, 17])
 def test_gemm_every_k_remainder(lib, cfg, fmt):
     """Every K-loop length from 1 to 7 K-steps (K = 64 .. 448), every epilogue, for each
     tile config -- 2: 256x128 (X ring NS 2), 3: 128x128, 4: 64x64, 5: 128x256 (NS 4), 6:
     64x64 with the 4-set weight ring (WR 4), 7: 64x64 on 4 waves (2 along the tokens), 8: 64x32
     on 2 waves along the tokens, 11: 256x128 with the X pieces in one burst in front of the
-    MFMAs (2 interleaves them), 13 / 14 / 15: 3 / 4 / 7 with interleaved X pieces -- so every remainder of the unrolled K loop
+    MFMAs (2 interleaves them), 13 / 14 / 15: 3 / 4 / 7 with interleaved X pieces, 16 / 17: 7 / 4
+    with wave-private X rings (no barrier in the K loop) -- so every remainder of the unrolled K loop
     (triples for WR 3, quadruples for WR 4) and every prologue clamp runs against numpy.
     The waits these paths rely on are derived, not hand-counted (gemm.hip z_waits)."""
-    N = {2: 256, 3: 256, 4: 128, 5: 256, 6: 128, 7: 128, 8: 96, 11: 256, 13: 256, 14: 128, 15: 128}[cfg]
+    N = {2: 256, 3: 256, 4: 128, 5: 256, 6: 128, 7: 128, 8: 96, 11: 256, 13: 256, 14: 128, 15: 128, 16: 128, 17: 128}[cfg]
     M = 256
     for ks in range(1, 8):
         K = 64 * ks
@@ -318,13 +319,14 @@ def test_attention_matches_numpy(lib, variant, dh):
 
 
 @pytest.mark.parametrize("fmt", [1, 2, 3, 8])
-@pytest.mark.parametrize("cfg", [2, 3, 7, 8, 11, 13, 14, 15])
+@pytest.mark.parametrize("cfg", [2, 3, 7, 8, 11, 13, 14, 15, 16, 17])
 def test_small_tiles_bitwise_equal_to_64x64(lib, fmt, cfg):
     """Waves along the tokens change who computes an output, not how: every (token,
     feature) is the same k-ordered MFMA chain and the same epilogue arithmetic, so
     configs 7 and 8 give the 64x64 tile's bits (the forward's batch-composition
     invariance rests on it), including the residual form's LN statistics; so do the
-    256- and 128-row tiles and the interleaved-X forms (2, 3, 11, 13-15)."""
+    256- and 128-row tiles, the interleaved-X forms (2, 3, 11, 13-15) and the
+    wave-private rings (16, 17)."""
     N, K, M = 768, 1536, 256
     rng = np.random.default_rng(fmt + cfg)
     W = rng.standard_normal((N, K)).astype(np.float32) * 0.05
