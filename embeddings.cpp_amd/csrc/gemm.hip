@@ -103,24 +103,38 @@ struct ZSet {
 // ahead of their 2 FA MFMAs (a ring of PF + 1 fragments); A fragments
 // dequantized from the register set `cur` (s = 0 first half, s = 1 second);
 // acc[2 f + a] = features +32 f + 16 a.
-template <int NJ, int FA, int PF, class R, class H, int... I>
+// The first PF B-fragment reads of a K-step (zmma_items issues them itself
+// unless PRE: then the caller issued them earlier with zmma_pre).
+template <int NJ, int PF, int... I>
+__device__ __forceinline__ void zmma_pre(h16x8 (&bq)[PF + 1], uint32_t b0, uint32_t b1, std::integer_sequence<int, I...>)
+{
+    auto rd = [&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        if constexpr (i < PF && i < 2 * NJ) bq[i % (PF + 1)] = zds_read<(i % NJ) << 11>(i < NJ ? b0 : b1);
+    };
+    (rd(std::integral_constant<int, I>{}), ...);
+}
+
+// ALLDQ: all four A fragments of a 32-feature group dequantized up front (short
+// K-steps, where the mid-step dequantization sat on the critical path), else
+// the second k-slice's at item NJ (fewer live registers).
+template <int NJ, int FA, int PF, bool PRE, bool ALLDQ, class R, class H, int... I>
 __device__ __forceinline__ void zmma_items(const R &cur, uint32_t b0, uint32_t b1, f32x4 (&acc)[2 * FA][NJ],
-                                           const H &hook, std::integer_sequence<int, I...>)
+                                           const H &hook, h16x8 (&bq)[PF + 1], std::integer_sequence<int, I...> seq)
 {
     constexpr int NI = 2 * NJ;
-    h16x8 bq[PF + 1];
     auto rd = [&](auto ic) {
         constexpr int i = decltype(ic)::value;
         if constexpr (i < NI) bq[i % (PF + 1)] = zds_read<(i % NJ) << 11>(i < NJ ? b0 : b1);
     };
-    auto pre = [&](auto ic) {
-        constexpr int i = decltype(ic)::value;
-        if constexpr (i < PF) rd(std::integral_constant<int, i>{});
-    };
-    (pre(std::integral_constant<int, I>{}), ...);
-    h16x8 af[2 * FA];
+    if constexpr (!PRE) zmma_pre<NJ, PF>(bq, b0, b1, seq);
+    h16x8 af[2 * FA], af2[ALLDQ ? 2 * FA : 1];
 #pragma unroll
     for (int f = 0; f < FA; ++f) { af[2 * f] = cur.r[f].frag(0); af[2 * f + 1] = cur.r[f].frag(2); }
+    if constexpr (ALLDQ) {
+#pragma unroll
+        for (int f = 0; f < FA; ++f) { af2[2 * f] = cur.r[f].frag(1); af2[2 * f + 1] = cur.r[f].frag(3); }
+    }
     auto item = [&](auto ic) {
         constexpr int i = decltype(ic)::value;
         hook(ic);                                     // (XI: an X piece of the next stage)
@@ -128,8 +142,13 @@ __device__ __forceinline__ void zmma_items(const R &cur, uint32_t b0, uint32_t b
         constexpr int last = (i + PF < NI ? i + PF : NI - 1);
         zwait_lgkm<last - i>(bq[i % (PF + 1)]);
         if constexpr (i == NJ) {
+            if constexpr (ALLDQ) {
 #pragma unroll
-            for (int f = 0; f < FA; ++f) { af[2 * f] = cur.r[f].frag(1); af[2 * f + 1] = cur.r[f].frag(3); }
+                for (int u = 0; u < 2 * FA; ++u) af[u] = af2[u];
+            } else {
+#pragma unroll
+                for (int f = 0; f < FA; ++f) { af[2 * f] = cur.r[f].frag(1); af[2 * f + 1] = cur.r[f].frag(3); }
+            }
         }
         const h16x8 bf = bq[i % (PF + 1)];
 #pragma unroll
@@ -408,35 +427,6 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     auto kstep = [&](ZSet<FMT, FA> &cur, ZSet<FMT, FA> &nxt, int ks, auto tail) {
         const int kx = min(ks + NS - 1, KS - 1), kw = min(ks + WR - 1, KS - 1);
         const int sx = st == 0 ? NS - 1 : st - 1;
-        if constexpr (XMODE) {
-            wload_or_tail(nxt, kw, tail);
-            wait_vmcnt<ZW.front>();
-        } else if constexpr (NS == 2 && !PRIV) {
-#ifdef GEMM_STAMPS
-            // (NS 2: slot 6 holds the cycles of the X pieces' issue instead of the front wait)
-            const unsigned long long zd = __builtin_amdgcn_s_memtime();
-#endif
-            issue_x(kx, sx);
-            asm volatile("" ::: "memory");
-#ifdef GEMM_STAMPS
-            zw_front += __builtin_amdgcn_s_memtime() - zd;
-#endif
-            wload_or_tail(nxt, kw, tail);
-            wait_vmcnt<ZW.front>();
-        } else {
-            wload_or_tail(nxt, kw, tail);
-            asm volatile("" ::: "memory");
-            issue_x(kx, sx);
-#ifdef GEMM_STAMPS
-            const unsigned long long za = __builtin_amdgcn_s_memtime();
-#endif
-            wait_vmcnt<ZW.front>();
-#ifdef GEMM_STAMPS
-            zw_front += __builtin_amdgcn_s_memtime() - za;
-#endif
-        }
-        cur.pin_all();
-        const uint32_t xs = lds_u32(smem + (PRIV ? (wave * NS + st) * XBW : st * XB) + rbase);
         // XI: X(ks + 1)'s XG pieces among the first XG * XS items (one every XS), so
         // the CU's texture path takes a wave's pieces between its MFMAs instead of
         // in one burst in front of them
@@ -445,16 +435,67 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
             constexpr int i = decltype(ic)::value;
             if constexpr (XMODE && i % XS == 0 && i / XS < XG) issue_x_piece(kx, sx, i / XS);
         };
-        zmma_items<NJ, FA, PF>(cur, xs + ((g ^ sw) << 4), xs + (((4 + g) ^ sw) << 4), acc, hook,
-                       std::make_integer_sequence<int, 2 * NJ>{});
+        if constexpr (PRIV) {
+            // private rings: X(ks) was retired by this wave's previous back wait (or
+            // the prologue), so the step's B reads go out before its loads and front
+            // wait (their latency under the wait), and all four A fragments are
+            // dequantized up front; nothing between the reads and the items'
+            // lgkmcnt waits may use the LDS / scalar-memory counter
+            const uint32_t xs = lds_u32(smem + (wave * NS + st) * XBW + rbase);
+            const uint32_t b0 = xs + ((g ^ sw) << 4), b1 = xs + (((4 + g) ^ sw) << 4);
+            h16x8 bq[PF + 1];
+            zmma_pre<NJ, PF>(bq, b0, b1, std::make_integer_sequence<int, 2 * NJ>{});
+            wload_or_tail(nxt, kw, tail);
+            if constexpr (!XMODE) {
+                asm volatile("" ::: "memory");
+                issue_x(kx, sx);
+            }
+            wait_vmcnt<ZW.front>();
+            cur.pin_all();
+            zmma_items<NJ, FA, PF, true, true>(cur, b0, b1, acc, hook, bq, std::make_integer_sequence<int, 2 * NJ>{});
+            wait_vmcnt<ZW.back>();
+        } else {
+            if constexpr (XMODE) {
+                wload_or_tail(nxt, kw, tail);
+                wait_vmcnt<ZW.front>();
+            } else if constexpr (NS == 2) {
 #ifdef GEMM_STAMPS
-        const unsigned long long zb = __builtin_amdgcn_s_memtime();
+                // (NS 2: slot 6 holds the cycles of the X pieces' issue instead of the front wait)
+                const unsigned long long zd = __builtin_amdgcn_s_memtime();
 #endif
-        wait_vmcnt<ZW.back>();
-        if constexpr (!PRIV) lds_barrier();
+                issue_x(kx, sx);
+                asm volatile("" ::: "memory");
 #ifdef GEMM_STAMPS
-        zw_back += __builtin_amdgcn_s_memtime() - zb;
+                zw_front += __builtin_amdgcn_s_memtime() - zd;
 #endif
+                wload_or_tail(nxt, kw, tail);
+                wait_vmcnt<ZW.front>();
+            } else {
+                wload_or_tail(nxt, kw, tail);
+                asm volatile("" ::: "memory");
+                issue_x(kx, sx);
+#ifdef GEMM_STAMPS
+                const unsigned long long za = __builtin_amdgcn_s_memtime();
+#endif
+                wait_vmcnt<ZW.front>();
+#ifdef GEMM_STAMPS
+                zw_front += __builtin_amdgcn_s_memtime() - za;
+#endif
+            }
+            cur.pin_all();
+            const uint32_t xs = lds_u32(smem + st * XB + rbase);
+            h16x8 bq[PF + 1];
+            zmma_items<NJ, FA, PF, false, false>(cur, xs + ((g ^ sw) << 4), xs + (((4 + g) ^ sw) << 4), acc, hook, bq,
+                                                 std::make_integer_sequence<int, 2 * NJ>{});
+#ifdef GEMM_STAMPS
+            const unsigned long long zb = __builtin_amdgcn_s_memtime();
+#endif
+            wait_vmcnt<ZW.back>();
+            lds_barrier();
+#ifdef GEMM_STAMPS
+            zw_back += __builtin_amdgcn_s_memtime() - zb;
+#endif
+        }
         st = st == NS - 1 ? 0 : st + 1;
     };
     int ks = 0;

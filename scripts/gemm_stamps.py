@@ -23,9 +23,9 @@ buf = (ctypes.c_ulonglong * n)()
 L.bertx_gemm_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
 assert L.bertx_gemm_stamps(buf, n) == 0
 a = np.frombuffer(buf, dtype=np.uint64).reshape(-1, 8).astype(np.int64)
-nw = 8 if cfg in (9, 10) else 4 if cfg in (2, 3, 5, 0) else 2
-bm = {2: 256, 3: 128, 4: 64, 5: 128}.get(cfg, 256)
-bn = 256 if cfg == 5 else 32 * nw
+nw = 4 if cfg in (2, 3, 5, 0, 7, 11, 13, 15, 16, 19) else 2
+bm = {2: 256, 3: 128, 4: 64, 5: 128, 7: 64, 14: 64, 15: 64, 16: 64, 17: 64, 19: 64, 20: 64, 6: 64, 8: 64}.get(cfg, 256)
+bn = 256 if cfg == 5 else 32 * nw // (2 if cfg in (7, 8, 15, 16, 19) else 1)
 tiles = (M // bm) * ((N + bn - 1) // bn)
 a = a[:tiles * nw]
 print(f"N={N} K={K} epi={epi} cfg={cfg} M={M}: {us.value:.1f} us, {tiles} tiles", flush=True)

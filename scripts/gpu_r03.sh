@@ -80,6 +80,11 @@ if has xismall; then
     python3 -c "import json; d=json.loads(open('$OUT/xismall_${e}_${r}.log').read().strip().splitlines()[-1]); p=d['probes']; print('xi=$e', 'C3', d['value'], 'C2', p['f16_mfma']['sentences_per_s'], 'B1', p['q4_0_hbm']['latency_us'])" | tee -a $OUT/xismall.log
   done; done
 fi
+if has b1stamp; then
+  for a in "2304 768 0" "768 768 2" "3072 768 1" "768 3072 2"; do SWEEP_M=64 STAMPS_LIB=build/stamps/libbert.so step 120 python -u scripts/gemm_stamps.py $a ${B1CFG:-16} >> $OUT/b1_stamps.log 2>&1 || exit 1; done
+  ( cd /tmp && step 200 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/b1prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/scripts/b1_trace.py 32 50 > $GRAFT_REPO_ROOT/$OUT/b1_trace.log 2>&1 ) || exit 1
+  cat $OUT/b1_stamps.log
+fi
 if has tok; then step 300 python -u scripts/host_throughput.py tok --texts 4000 > $OUT/tok.log 2>&1 || exit 1; fi
 if has server; then step 400 python -u scripts/host_throughput.py server > $OUT/server.log 2>&1 || { tail -20 $OUT/server.log; exit 1; }; fi
 echo session-ok
