@@ -669,7 +669,13 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
                         for (int e = 0; e < 4; ++e)
                             pw[e] = __builtin_bit_cast(uint32_t, h16x2{(h16)v[a][2 * e], (h16)v[a][2 * e + 1]});
                     }
-                    *(uint4 *)((h16 *)out + (size_t)tok * N + cb + 16 * a) = pk;
+                    h16 *const dst = (h16 *)out + (size_t)tok * N + cb + 16 * a;
+                    if (ln.store_nt) {
+                        typedef uint32_t u32x4n __attribute__((ext_vector_type(4)));
+                        __builtin_nontemporal_store(__builtin_bit_cast(u32x4n, pk), (u32x4n *)dst);
+                    } else {
+                        *(uint4 *)dst = pk;
+                    }
                 }
             }
         }
@@ -727,7 +733,7 @@ void dispatch_z(const DevWeight &W, const h16 *x, int M, const float *bias, int 
 
 template <int FMT>
 void launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, int32_t epi, const void *res,
-                void *out, hipStream_t s, const LnFold &ln, bool lnf, int cfg)
+                void *out, hipStream_t s, LnFold ln, bool lnf, int cfg)
 {
     if (cfg == 0) {
         // the largest tile that still gives every CU work: 256 x 128 tiles two per CU
@@ -750,6 +756,13 @@ void launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, 
         static const bool xi_env = [] { const char *e = std::getenv("BERT_GEMM_XI"); return e && *e == '1'; }();
         if (xi_env) cfg = cfg == 3 ? 13 : cfg == 4 ? 14 : cfg == 7 ? 15 : cfg;
     }
+    // Non-temporal output stores on the 256-row tiles (large batches): the output
+    // streams past L2 instead of evicting the X panels the next column tiles read
+    // (C3: FFN-down 143 -> 140 us, QKV -1 us, forward +0.5 %, alternating on one
+    // box, profiles/r03_attention_flow_ab.log nt rows); the small forms keep L2
+    // stores (their next kernel reads the output while it is still there).
+    // BERT_GEMM_NT = 0 / 1 forces it off / on everywhere.
+    if (ln.store_nt < 0) ln.store_nt = (cfg == 2 || cfg == 11) ? 1 : 0;
     // 256 x 128: the X pieces among the MFMAs (one per B-fragment item from the
     // K-step's start; +1.2-1.6 % on the C3 forward over one burst in front of them,
     // profiles/r03_gemm_xi_ab.log); cfg 11 keeps the burst form for A/B
@@ -809,14 +822,17 @@ int launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *b
     if (epi == EPI_BIAS_RES && !res_ln && (ln.res_stats || ln.g_next)) return -1;
     if (epi != EPI_BIAS_RES && ln.in_stats && !ln.c1) return -1;
     const bool lnf = epi == EPI_BIAS_RES ? res_ln : ln.in_stats != nullptr;
+    static const int nt_env = [] { const char *e = std::getenv("BERT_GEMM_NT"); return e ? std::atoi(e) : -1; }();
+    LnFold lnx = ln;
+    lnx.store_nt = nt_env;
     // A/B hook: BERT_GEMM_CFG forces a tile config in the forward (tests/benches set g_gemm_cfg)
     static const int env_cfg = [] { const char *e = std::getenv("BERT_GEMM_CFG"); return e ? std::atoi(e) : 0; }();
     const int cfg = g_gemm_cfg ? g_gemm_cfg : env_cfg;
     switch (W.fmt) {
-    case FMT_Q4_0: launch_fmt<FMT_Q4_0>(W, x, M, bias, epi, res, out, s, ln, lnf, cfg); break;
-    case FMT_Q4_1: launch_fmt<FMT_Q4_1>(W, x, M, bias, epi, res, out, s, ln, lnf, cfg); break;
-    case FMT_Q8_0: launch_fmt<FMT_Q8_0>(W, x, M, bias, epi, res, out, s, ln, lnf, cfg); break;
-    default: launch_fmt<FMT_F16>(W, x, M, bias, epi, res, out, s, ln, lnf, cfg); break;
+    case FMT_Q4_0: launch_fmt<FMT_Q4_0>(W, x, M, bias, epi, res, out, s, lnx, lnf, cfg); break;
+    case FMT_Q4_1: launch_fmt<FMT_Q4_1>(W, x, M, bias, epi, res, out, s, lnx, lnf, cfg); break;
+    case FMT_Q8_0: launch_fmt<FMT_Q8_0>(W, x, M, bias, epi, res, out, s, lnx, lnf, cfg); break;
+    default: launch_fmt<FMT_F16>(W, x, M, bias, epi, res, out, s, lnx, lnf, cfg); break;
     }
     return 0;
 }

@@ -85,6 +85,15 @@ if has b1stamp; then
   ( cd /tmp && step 200 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/b1prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/scripts/b1_trace.py 32 50 > $GRAFT_REPO_ROOT/$OUT/b1_trace.log 2>&1 ) || exit 1
   cat $OUT/b1_stamps.log
 fi
+if has ntab; then
+  # non-temporal output stores of the 256-row GEMM tiles (default) vs plain stores (BERT_GEMM_NT=0), alternating
+  for r in 1 2; do
+    for n in -1 0; do
+      BERT_GEMM_NT=$n step 200 python -u bench.py --no-cpu-baseline --no-probes --no-library --no-pmc > $OUT/ntab_${n}_${r}.log 2>&1 || exit 1
+      python3 -c "import json; d=json.loads(open('$OUT/ntab_${n}_${r}.log').read().strip().splitlines()[-1]); print('nt=$n', d['value'], {k: round(v['avg_us'],1) for k,v in d['kernels'].items()})" | tee -a $OUT/ntab.log
+    done
+  done
+fi
 if has tok; then step 300 python -u scripts/host_throughput.py tok --texts 4000 > $OUT/tok.log 2>&1 || exit 1; fi
 if has server; then step 400 python -u scripts/host_throughput.py server > $OUT/server.log 2>&1 || { tail -20 $OUT/server.log; exit 1; }; fi
 echo session-ok
