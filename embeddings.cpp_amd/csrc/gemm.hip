@@ -758,8 +758,9 @@ void launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, 
     }
     // Non-temporal output stores on the 256-row tiles (large batches): the output
     // streams past L2 instead of evicting the X panels the next column tiles read
-    // (C3: FFN-down 143 -> 140 us, QKV -1 us, forward +0.5 %, alternating on one
-    // box, profiles/r03_attention_flow_ab.log nt rows); the small forms keep L2
+    // (C3: FFN-down 143 -> 140 us, QKV -1 us, forward +0.5 % alternating on one box,
+    // profiles/r03_attention_flow_ab.log nt rows; noise on another, r03_gemm_w8_nt_ab.log);
+    // the small forms keep L2
     // stores (their next kernel reads the output while it is still there).
     // BERT_GEMM_NT = 0 / 1 forces it off / on everywhere.
     if (ln.store_nt < 0) ln.store_nt = (cfg == 2 || cfg == 11) ? 1 : 0;
