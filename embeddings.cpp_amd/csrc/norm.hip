@@ -8,6 +8,7 @@
 #include "table_read.h"
 
 #include <cmath>
+#include <cstdlib>
 
 namespace emb {
 
@@ -204,23 +205,28 @@ __global__ __launch_bounds__(256) void pool_final_kernel(const float *__restrict
     pool_normalize(part + (size_t)b * n_chunks * d, d, n_chunks, out + (size_t)b * d);
 }
 
-// Batches of at most one chunk (max_len <= 64): both stages in one launch, the
-// column sums through LDS instead of HBM, the same arithmetic as the two
-// kernels above (so the same bits).
+// Batches of at most POOL_ONE_MAX chunks (max_len <= 256): both stages in one
+// launch, a sentence's chunks summed one after another by its workgroup and the
+// column sums kept in LDS instead of HBM -- the same arithmetic and order as the
+// two kernels above (so the same bits), one launch fewer (C2: L 128).
+constexpr int POOL_ONE_MAX = 4;
 __global__ __launch_bounds__(256) void pool_one_kernel(const h16 *__restrict__ z, const float2 *__restrict__ stats,
                                                        const float *__restrict__ lw, const float *__restrict__ lb,
-                                                       const int32_t *__restrict__ cu, int d, float *__restrict__ out)
+                                                       const int32_t *__restrict__ cu, int d, int n_chunks,
+                                                       float *__restrict__ out)
 {
-    __shared__ __attribute__((aligned(16))) float cs[1024];
+    __shared__ __attribute__((aligned(16))) float cs[POOL_ONE_MAX * 1024];
     const int b = blockIdx.x, tid = threadIdx.x;
-    f32x4 s0, s1;
-    pool_chunk_sum(z, stats, lw, lb, cu, d, b, 0, s0, s1);
-    if (tid < d / 8) {
-        *(f32x4 *)(cs + 8 * tid) = s0;
-        *(f32x4 *)(cs + 8 * tid + 4) = s1;
+    for (int ch = 0; ch < n_chunks; ++ch) {
+        f32x4 s0, s1;
+        pool_chunk_sum(z, stats, lw, lb, cu, d, b, ch, s0, s1);
+        if (tid < d / 8) {
+            *(f32x4 *)(cs + ch * d + 8 * tid) = s0;
+            *(f32x4 *)(cs + ch * d + 8 * tid + 4) = s1;
+        }
+        __syncthreads();   // pool_chunk_sum's reduction buffer is reused by the next chunk
     }
-    __syncthreads();
-    pool_normalize(cs, d, 1, out + (size_t)b * d);
+    pool_normalize(cs, d, n_chunks, out + (size_t)b * d);
 }
 
 // diagnostics (BERT_CHECK_FINITE): count non-finite values of a buffer
@@ -276,8 +282,10 @@ void launch_pool_l2(const uint16_t *z, const float2 *stats, const float *ln_w, c
                     int32_t n_seqs, int32_t max_len, int32_t d, float *partial, float *out, hipStream_t s)
 {
     const int nc = pool_chunks(max_len);
-    if (nc == 1) {
-        pool_one_kernel<<<n_seqs, 256, 0, s>>>((const h16 *)z, stats, ln_w, ln_b, cu, d, out);
+    // BERT_POOL_ONE=0: the two launches for every batch (A/B)
+    static const bool one = [] { const char *e = std::getenv("BERT_POOL_ONE"); return !(e && *e == '0'); }();
+    if (nc == 1 || (one && nc <= POOL_ONE_MAX && d <= 1024)) {
+        pool_one_kernel<<<n_seqs, 256, 0, s>>>((const h16 *)z, stats, ln_w, ln_b, cu, d, nc, out);
         return;
     }
     pool_partial_kernel<<<dim3(nc, n_seqs), 256, 0, s>>>((const h16 *)z, stats, ln_w, ln_b, cu, d, nc, partial);

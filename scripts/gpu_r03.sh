@@ -94,6 +94,20 @@ if has ntab; then
     done
   done
 fi
+if has c2sweep; then
+  # every GEMM on one tile config (BERT_GEMM_CFG) against the heuristic (0): the small-batch probes
+  for c in ${SWEEPC:-0 3 4 7 13 14 16 0}; do
+    BERT_GEMM_CFG=$c step 300 python -u bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-library --no-pmc > $OUT/c2sweep_${c}.log 2>&1 || exit 1
+    python3 -c "import json; d=json.loads(open('$OUT/c2sweep_${c}.log').read().strip().splitlines()[-1]); p=d['probes']; print('cfg=$c', 'C2', p['f16_mfma']['sentences_per_s'], p['f16_mfma']['kernel_avg_us'], 'B1', p['q4_0_hbm']['latency_us'])" | tee -a $OUT/c2sweep.log
+  done
+fi
+if has poolab; then
+  # one-launch pool over <= 4 chunks (default) vs the two launches (BERT_POOL_ONE=0), alternating: C2 probe
+  for r in 1 2; do for e in 1 0; do
+    BERT_POOL_ONE=$e step 300 python -u bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-library --no-pmc > $OUT/poolab_${e}_${r}.log 2>&1 || exit 1
+    python3 -c "import json; d=json.loads(open('$OUT/poolab_${e}_${r}.log').read().strip().splitlines()[-1]); p=d['probes']; print('pool_one=$e', 'C2', p['f16_mfma']['sentences_per_s'], p['f16_mfma']['kernel_avg_us'], 'B1', p['q4_0_hbm']['latency_us'])" | tee -a $OUT/poolab.log
+  done; done
+fi
 if has tok; then step 300 python -u scripts/host_throughput.py tok --texts 4000 > $OUT/tok.log 2>&1 || exit 1; fi
 if has server; then step 400 python -u scripts/host_throughput.py server > $OUT/server.log 2>&1 || { tail -20 $OUT/server.log; exit 1; }; fi
 echo session-ok
