@@ -33,11 +33,39 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(DevTable word, DevTable t
                                                        const int32_t *__restrict__ cu, int d, h16 *__restrict__ z,
                                                        float2 *__restrict__ stats)
 {
+    // the block's 16 rows pos + (type[0] + word[id]) (bert.cpp:968-973 operand
+    // order, f32) staged in LDS by whole quant blocks -- (row, 32-column block)
+    // items over the 256 threads, a few wide loads each instead of three narrow
+    // loads per 4 values -- then read back by the row groups below
+    extern __shared__ __attribute__((aligned(16))) float vs[];   // [16][d]
     const int b = blockIdx.y, l16 = threadIdx.x & 15;
-    const int i = blockIdx.x * 16 + (threadIdx.x >> 4);
     const int start = cu[b], len = cu[b + 1] - start;
+    {
+        const int nb = d / 32;
+        for (int it = threadIdx.x; it < 16 * nb; it += 256) {
+            const int r = it / nb, k = it - r * nb, ii = blockIdx.x * 16 + r;
+            float v[32];
+            if (ii < len) {
+                float w[32], ty[32], p[32];
+                table32(word, ids[start + ii], k, w);
+                table32(type, 0, k, ty);
+                table32(pos, ii, k, p);
+#pragma unroll
+                for (int e = 0; e < 32; ++e) v[e] = p[e] + (ty[e] + w[e]);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 32; ++e) v[e] = 0.f;   // rows past the sentence: never stored
+            }
+            f32x4 *dst = (f32x4 *)(vs + r * d + 32 * k);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) dst[q] = f32x4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+        }
+        __syncthreads();
+    }
+    const int i = blockIdx.x * 16 + (threadIdx.x >> 4);
     const bool ok = i < len;                       // whole 16-lane groups: the shuffles stay in-group
-    const int t = start + (ok ? i : 0), id = ok ? ids[t] : 0;
+    const int t = start + (ok ? i : 0);
+    const float *vrow = vs + (threadIdx.x >> 4) * d;
     const int ns = d / 64;
     f32x4 v[EMB_MAXS];
     float s = 0.f;
@@ -45,10 +73,7 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(DevTable word, DevTable t
     for (int k = 0; k < EMB_MAXS; ++k) {
         if (k < ns) {
             const int c = 4 * (l16 + 16 * k);
-            // pos + (type[0] + word[id])  (bert.cpp:968-973 operand order), f32
-            const f32x4 w = table4(word, id, c), ty = table4(type, 0, c), p = table4(pos, ok ? i : 0, c);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[k][e] = p[e] + (ty[e] + w[e]);
+            v[k] = *(const f32x4 *)(vrow + c);
             s += (v[k][0] + v[k][1]) + (v[k][2] + v[k][3]);
         }
     }
@@ -252,7 +277,7 @@ void launch_embed_ln(const DevTable &word, const DevTable &type, const DevTable 
                      float2 *stats, hipStream_t s)
 {
     dim3 grid((max_len + 15) / 16, n_seqs);
-    embed_ln_kernel<<<grid, 256, 0, s>>>(word, type, pos, ln_w, ids, cu, d, (h16 *)z, stats);
+    embed_ln_kernel<<<grid, 256, (size_t)16 * d * 4, s>>>(word, type, pos, ln_w, ids, cu, d, (h16 *)z, stats);
 }
 
 int launch_ln_stats(const float2 *part, int32_t G, int32_t stride, int32_t rows, int32_t d, float2 *stats,
