@@ -224,12 +224,27 @@ def pmc_pass(model_path, B, L, counter, steps, warmup, timeout_s, device):
         shutil.rmtree(out, ignore_errors=True)
 
 
+def under_profiler(env=None):
+    """True when this process already runs under a profiler (rocprofv3 preloads its
+    tool library and exports ROCP*/ROCPROF* variables into the profiled program).
+    Starting rocprofv3 (a #!/usr/bin/env python3 script) from such a process is an
+    exec from a GPU-initialised process tree, which this pool refuses."""
+    env = os.environ if env is None else env
+    pre = env.get("LD_PRELOAD", "")
+    if re.search(r"roctracer|rocprof|rocprofiler|libroctx|rocm_sdk", pre, re.I):
+        return True
+    return any(k.startswith(("ROCP_", "ROCPROF", "ROCPROFILER", "ROCTX", "ROCP_TOOL")) for k in env)
+
+
 def pmc_live(model_path, B, L, device=0, steps=2, warmup=1, timeout_s=120):
     """This run's HBM-side traffic of one forward of B x L tokens, per kernel class:
     2 x FETCH_SIZE + WRITE_SIZE (KiB -> B; gfx950 FETCH_SIZE counts half the bytes of
     16-B-per-lane reads, MI355X_MICROARCH.md "HBM"), from two rocprofv3 --pmc passes
     (the two counters cannot share a pass) over build/bin/bert_probe.  Infinity-Cache
-    hits are included, so this is an upper bound on DRAM bytes."""
+    hits are included, so this is an upper bound on DRAM bytes.  Under a profiler
+    (under_profiler) nothing is started: the result says so."""
+    if under_profiler():
+        return {"skipped": "under a profiler (rocprofv3 preload in this process): no nested rocprofv3 passes"}
     t0 = time.perf_counter()
     fetch = pmc_pass(model_path, B, L, "FETCH_SIZE", steps, warmup, timeout_s, device)
     write = pmc_pass(model_path, B, L, "WRITE_SIZE", steps, warmup, timeout_s, device)
@@ -287,7 +302,8 @@ def probes(lib, bertpy, torch, a, dev, stream, q4_path):
     if not a.no_pmc:
         try:
             pm = pmc_live(p2, 32, 128, device=int(os.environ.get("LOCAL_RANK", "0")))
-            pm["gbps_at_measured_step"] = round(pm["bytes_per_forward"] / (el / steps) / 1e9, 1)
+            if "bytes_per_forward" in pm:
+                pm["gbps_at_measured_step"] = round(pm["bytes_per_forward"] / (el / steps) / 1e9, 1)
             out["f16_mfma"]["pmc"] = pm
         except Exception as ex:   # a report, never the metric
             out["f16_mfma"]["pmc"] = {"error": str(ex)}
@@ -317,8 +333,9 @@ def probes(lib, bertpy, torch, a, dev, stream, q4_path):
     if not a.no_pmc:
         try:
             pm = pmc_live(q4_path, 1, 32, device=int(os.environ.get("LOCAL_RANK", "0")), steps=3)
-            gbps = pm["bytes_per_forward"] / lat / 1e9
-            pm.update({"counter_gbps": round(gbps, 2), "counter_hbm_frac": round(gbps / HBM_PEAK_GBPS, 5)})
+            if "bytes_per_forward" in pm:
+                gbps = pm["bytes_per_forward"] / lat / 1e9
+                pm.update({"counter_gbps": round(gbps, 2), "counter_hbm_frac": round(gbps / HBM_PEAK_GBPS, 5)})
             out["q4_0_hbm"]["pmc"] = pm
         except Exception as ex:
             out["q4_0_hbm"]["pmc"] = {"error": str(ex)}

@@ -72,6 +72,8 @@ def load_lib(path=None):
     L.bertx_device_last_call.restype = c_i32
     L.bertx_device_last_call.argtypes = [vp, c_i32, ctypes.POINTER(ctypes.c_double), c_i32p,
                                          ctypes.POINTER(ctypes.c_int64)]
+    L.bertx_device_calls.restype = ctypes.c_int64
+    L.bertx_device_calls.argtypes = [vp, c_i32]
     L.bertx_quantize_file.restype = c_i32
     L.bertx_quantize_file.argtypes = [ctypes.c_char_p, ctypes.c_char_p, c_i32]
     L.bertx_convert_hf.restype = c_i32
@@ -82,6 +84,8 @@ def load_lib(path=None):
     L.bertx_test_gemm.argtypes = [c_i32, c_i32, c_i32, vp, c_f32p, c_i32, vp, c_i32, vp, vp, c_i32]
     L.bertx_test_gemm_ln.restype = c_i32
     L.bertx_test_gemm_ln.argtypes = [c_i32, c_i32, c_i32, vp, vp, c_i32, vp, vp, vp, vp, c_i32] + [vp] * 7 + [c_i32]
+    L.bertx_test_gemm_ran.restype = c_i32
+    L.bertx_test_gemm_ran.argtypes = []
     L.bertx_test_gemm_f32.restype = c_i32
     L.bertx_test_gemm_f32.argtypes = [c_i32, c_i32, vp, vp, c_i32, vp, c_i32, vp, vp]
     L.bertx_bench_gemm.restype = c_i32

@@ -703,6 +703,7 @@ __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restr
             else wait_all_vm();
         }
         ASTAMP(5, __builtin_amdgcn_s_memtime());
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // no LDS read in flight into the store phase
         __syncthreads();                                  // S: region B is free
         if (LATE_STORE && active) store_rows();           // production: all waves store after S
         ASTAMP(6, __builtin_amdgcn_s_memtime());

@@ -12,9 +12,12 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <functional>
 #include <memory>
 #include <numeric>
 #include <string>
@@ -23,17 +26,79 @@
 
 using emb::Device;
 
+namespace {
+
+// A persistent host thread per replica (multi-replica contexts): run_forward posts
+// a replica's share of a call to it instead of creating a std::thread per call.
+class ReplicaWorker {
+public:
+    ReplicaWorker() : th_([this] { loop(); }) {}
+    ~ReplicaWorker()
+    {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_one();
+        th_.join();
+    }
+    void post(std::function<void()> f)
+    {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            q_.push_back(std::move(f));
+        }
+        cv_.notify_one();
+    }
+
+private:
+    void loop()
+    {
+        for (;;) {
+            std::function<void()> f;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+                if (q_.empty()) return;   // stop_ with nothing queued
+                f = std::move(q_.front());
+                q_.pop_front();
+            }
+            f();
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<std::function<void()>> q_;
+    bool stop_ = false;
+    std::thread th_;
+};
+
+}  // namespace
+
 struct bert_ctx {
     emb::HParams hp;
     emb::Vocab vocab;
     std::vector<std::unique_ptr<Device>> devices;
     bool host_only = false;
+    // routing state of run_forward: the cost of the work routed to each replica and
+    // not yet finished, and the rotation that breaks ties between equal loads
+    std::mutex route_mu;
+    std::vector<double> inflight;
+    unsigned rr = 0;
+    // declared after `devices`: destroyed (joined) before the replicas they drive
+    std::vector<std::unique_ptr<ReplicaWorker>> workers;
 };
 
 namespace {
 
 constexpr int64_t kChunkTokens = 1 << 17;   // tokens per device forward (workspace bound)
 constexpr int kChunkSeqs = 4096;            // sentences per device forward (pool / output staging bound)
+// A call is split over k replicas only when each share keeps at least this many
+// tokens: below it a forward is launch- and latency-bound (C2's 4,096 tokens run in
+// 0.37 ms, B = 1 in 0.56 ms), so splitting a small batch buys little latency and
+// costs every replica a forward; it goes whole to the least-loaded replica instead,
+// and concurrent callers (the server's batchers) land on different replicas.
+constexpr int64_t kMinShareTokens = 8192;
 
 std::vector<int> parse_device_list(int n_visible)
 {
@@ -66,10 +131,14 @@ double sentence_cost(const emb::HParams &hp, int L)
     return (double)L * (8.0 * d * d + 4.0 * d * f) + 4.0 * (double)L * L * d;
 }
 
-// Runs n sentences on the context's GPUs.  Work is split by cost over devices
-// (longest-processing-time first); each device walks its sentences in length
-// order in chunks of <= kChunkTokens.  Results are independent of the split:
-// every kernel computes a sentence from its own tokens only.
+// Runs n sentences on the context's GPUs.  Routing (kMinShareTokens): the call
+// uses k = min(replicas, tokens / kMinShareTokens) (at least 1) replicas, the k
+// least-loaded by the cost still in flight on them (ties rotate, so consecutive
+// small calls spread over the replicas too); its sentences are split over those k
+// by cost, longest first to the least-loaded share (LPT).  Each replica walks its
+// sentences in chunks of <= kChunkTokens on its persistent worker thread (the
+// caller runs one share itself).  Results are independent of the routing and the
+// split: every kernel computes a sentence from its own tokens only.
 int run_forward(bert_ctx *ctx, const int32_t *const *toks, const int32_t *lens, float *const *outs, int n)
 {
     if (ctx->devices.empty()) {
@@ -81,12 +150,29 @@ int run_forward(bert_ctx *ctx, const int32_t *const *toks, const int32_t *lens, 
     std::vector<int> order((size_t)n);
     std::iota(order.begin(), order.end(), 0);
     std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return lens[a] > lens[b]; });
+    int64_t tokens = 0;
+    for (int i = 0; i < n; ++i) tokens += lens[i];
+    const int k = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)nd, (int64_t)n, tokens / kMinShareTokens}));
     std::vector<std::vector<int>> assign((size_t)nd);
     std::vector<double> load((size_t)nd, 0.0);
-    for (int idx : order) {
-        const int dv = (int)(std::min_element(load.begin(), load.end()) - load.begin());
-        assign[(size_t)dv].push_back(idx);
-        load[(size_t)dv] += sentence_cost(ctx->hp, lens[idx]);
+    std::vector<int> chosen((size_t)nd);
+    {
+        std::lock_guard<std::mutex> lk(ctx->route_mu);
+        std::iota(chosen.begin(), chosen.end(), 0);
+        const unsigned rot = ctx->rr;
+        std::stable_sort(chosen.begin(), chosen.end(), [&](int a, int b) {
+            if (ctx->inflight[(size_t)a] != ctx->inflight[(size_t)b]) return ctx->inflight[(size_t)a] < ctx->inflight[(size_t)b];
+            return (unsigned)(a - (int)rot + nd) % nd < (unsigned)(b - (int)rot + nd) % nd;
+        });
+        chosen.resize((size_t)k);
+        ctx->rr = (rot + (unsigned)k) % (unsigned)nd;
+        for (int idx : order) {
+            int best = chosen[0];
+            for (int dv : chosen) if (load[(size_t)dv] < load[(size_t)best]) best = dv;
+            assign[(size_t)best].push_back(idx);
+            load[(size_t)best] += sentence_cost(ctx->hp, lens[idx]);
+        }
+        for (int dv : chosen) ctx->inflight[(size_t)dv] += load[(size_t)dv];
     }
     std::vector<int> rcs((size_t)nd, 0);
     auto work = [&](int dv) {
@@ -121,22 +207,34 @@ int run_forward(bert_ctx *ctx, const int32_t *const *toks, const int32_t *lens, 
             toks_done += tok;
         }
     };
-    int used = 0;
-    for (int dv = 0; dv < nd; ++dv) used += assign[(size_t)dv].empty() ? 0 : 1;
-    if (used <= 1) {
-        for (int dv = 0; dv < nd; ++dv) if (!assign[(size_t)dv].empty()) work(dv);
+    auto finish = [&](int dv) {
+        std::lock_guard<std::mutex> lk(ctx->route_mu);
+        ctx->inflight[(size_t)dv] -= load[(size_t)dv];
+        if (ctx->inflight[(size_t)dv] < 0.5) ctx->inflight[(size_t)dv] = 0.0;   // no drift from float sums
+    };
+    std::vector<int> used;
+    for (int dv : chosen) if (!assign[(size_t)dv].empty()) used.push_back(dv);
+    if (used.size() <= 1 || ctx->workers.size() != (size_t)nd) {
+        for (int dv : used) { work(dv); finish(dv); }
     } else {
-        std::vector<std::thread> th;
-        for (int dv = 0; dv < nd; ++dv) if (!assign[(size_t)dv].empty()) th.emplace_back(work, dv);
-        for (auto &t : th) t.join();
-    }
-    for (int dv = 0; dv < nd; ++dv)
-        if (assign[(size_t)dv].empty()) {
-            // under the replica's mutex, like the busy replicas' stamps (bertx_device_last_call reads them)
-            Device &D = *ctx->devices[(size_t)dv];
-            std::lock_guard<std::mutex> lk(D.mutex());
-            D.set_last_call(0.0, 0, 0);
+        // the other shares on their replicas' persistent workers, the first on this thread
+        std::mutex mu;
+        std::condition_variable cv;
+        size_t left = used.size() - 1;
+        for (size_t i = 1; i < used.size(); ++i) {
+            const int dv = used[i];
+            ctx->workers[(size_t)dv]->post([&, dv] {
+                work(dv);
+                finish(dv);
+                std::lock_guard<std::mutex> lk(mu);
+                if (--left == 0) cv.notify_one();
+            });
         }
+        work(used[0]);
+        finish(used[0]);
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return left == 0; });
+    }
     for (int rc : rcs) if (rc != 0) {
         std::fprintf(stderr, "libbert: forward failed (%d)\n", rc);
         return rc;
@@ -147,16 +245,27 @@ int run_forward(bert_ctx *ctx, const int32_t *const *toks, const int32_t *lens, 
 // Tokenize n texts into ids[i * n_max ..] (lens[i] = bert_tokenize's count, which
 // may exceed n_max: bert.cpp:386-387) on up to n_threads threads of the persistent
 // pool; the stage bert_encode_batch runs first (bert.cpp:1402-1406, sequential in
-// the reference).  Blocks of 8 texts per task.
-void tokenize_all(const bert_ctx *ctx, int n_threads, int n, const char *const *texts, int32_t n_max, int32_t *ids,
+// the reference).  Blocks of 8 texts per task.  False (after a message) when a
+// task threw (e.g. bad_alloc growing a scratch buffer): nothing may unwind out of
+// the C ABI, and the caller leaves its outputs untouched, as on every refusal.
+bool tokenize_all(const bert_ctx *ctx, int n_threads, int n, const char *const *texts, int32_t n_max, int32_t *ids,
                   int32_t *lens)
 {
     const int64_t n_blocks = ((int64_t)n + 7) / 8;
-    emb::TaskPool::instance().run(n_blocks, n_threads, [&](int64_t blk) {
-        const int e = (int)std::min<int64_t>(n, 8 * blk + 8);
-        for (int i = (int)(8 * blk); i < e; ++i)
-            lens[i] = ctx->vocab.tokenize(texts[i], n_max, ids + (size_t)i * n_max, n_max);
-    });
+    try {
+        emb::TaskPool::instance().run(n_blocks, n_threads, [&](int64_t blk) {
+            const int e = (int)std::min<int64_t>(n, 8 * blk + 8);
+            for (int i = (int)(8 * blk); i < e; ++i)
+                lens[i] = ctx->vocab.tokenize(texts[i], n_max, ids + (size_t)i * n_max, n_max);
+        });
+    } catch (const std::exception &ex) {
+        std::fprintf(stderr, "libbert: tokenization failed: %s\n", ex.what());
+        return false;
+    } catch (...) {
+        std::fprintf(stderr, "libbert: tokenization failed\n");
+        return false;
+    }
+    return true;
 }
 
 void print_usage(char **argv, const bert_params &p)
@@ -247,6 +356,9 @@ struct bert_ctx *bert_load_from_file(const char *fname)
         }
         ctx->devices.push_back(std::move(d));
     }
+    ctx->inflight.assign(ctx->devices.size(), 0.0);
+    if (ctx->devices.size() > 1)
+        for (size_t i = 0; i < ctx->devices.size(); ++i) ctx->workers.emplace_back(new ReplicaWorker());
     std::printf("bert_load_from_file: MI355X engine on %zu HIP device(s)\n", ctx->devices.size());
     if (m.hp.ftype == emb::FMT_F32)
         std::printf("bert_load_from_file: f32 file: f32 activations x f32 weights on the f32 MFMA chain "
@@ -305,7 +417,7 @@ void bert_encode_batch(struct bert_ctx *ctx, int32_t n_threads, int32_t n_batch_
     const int32_t N = ctx->hp.n_max_tokens;
     std::vector<int32_t> ids((size_t)n_inputs * N);
     std::vector<int32_t> lens((size_t)n_inputs);
-    tokenize_all(ctx, n_threads > 0 ? n_threads : 1, n_inputs, texts, N, ids.data(), lens.data());
+    if (!tokenize_all(ctx, n_threads > 0 ? n_threads : 1, n_inputs, texts, N, ids.data(), lens.data())) return;
     // which inputs the reference's chunking refuses (bert.cpp:1408-1443)
     std::vector<char> ok((size_t)n_inputs, 1);
     if (n_batch_size == n_inputs || n_batch_size <= 0) {
@@ -422,6 +534,14 @@ int32_t bertx_device_last_call(struct bert_ctx *ctx, int32_t slot, double *wall_
     return 0;
 }
 
+int64_t bertx_device_calls(struct bert_ctx *ctx, int32_t slot)
+{
+    if (!ctx || slot < 0 || slot >= (int32_t)ctx->devices.size()) return -1;
+    Device &D = *ctx->devices[(size_t)slot];
+    std::lock_guard<std::mutex> lk(D.mutex());
+    return D.calls();
+}
+
 int32_t bertx_quantize_file(const char *fin, const char *fout, int32_t itype)
 {
     return emb::quantize_file(fin, fout, itype, false);
@@ -436,8 +556,7 @@ int32_t bertx_tokenize_batch(struct bert_ctx *ctx, int32_t n_threads, int32_t n_
                              int32_t n_max, int32_t *ids, int32_t *n_tokens)
 {
     if (!ctx || n_inputs < 0 || n_max <= 0 || (n_inputs > 0 && (!texts || !ids || !n_tokens))) return -1;
-    tokenize_all(ctx, n_threads > 0 ? n_threads : 1, n_inputs, texts, n_max, ids, n_tokens);
-    return 0;
+    return tokenize_all(ctx, n_threads > 0 ? n_threads : 1, n_inputs, texts, n_max, ids, n_tokens) ? 0 : -1;
 }
 
 const char *bertx_version(void) { return "embeddings.cpp_amd 0.1 (gfx950)"; }

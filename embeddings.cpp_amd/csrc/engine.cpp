@@ -289,6 +289,18 @@ void Device::upload(const HostModel &m)
         return r;
     };
     const TabIdx tw = table(m.word), tt = table(m.ttype), tp = table(m.pos);
+    // f32 chain: the era's fp16 GELU and exp tables, built on the host (libm) as
+    // ggml built them, indexed on the device by the f16 bits of the input
+    size_t i_gelu = 0, i_exp = 0;
+    if (f32_) {
+        std::vector<uint16_t> tg, te;
+        era_tables(tg, te);
+        Piece pg, pe;
+        pg.bytes.assign((const uint8_t *)tg.data(), (const uint8_t *)(tg.data() + tg.size()));
+        pe.bytes.assign((const uint8_t *)te.data(), (const uint8_t *)(te.data() + te.size()));
+        i_gelu = add(std::move(pg));
+        i_exp = add(std::move(pe));
+    }
     const size_t lnw = vec(m.ln_e_w), lnb = vec(m.ln_e_b);
     auto fold = [&](std::vector<const HostTensor *> parts, std::vector<const HostTensor *> bias,
                     const HostTensor &gamma, const HostTensor &beta, size_t &i1, size_t &i2) {
@@ -358,6 +370,10 @@ void Device::upload(const HostModel &m)
         r.qs = P(x.q); r.d = (const uint16_t *)P(x.d); r.m = (const uint16_t *)P(x.m);
         return r;
     };
+    if (f32_) {
+        gelu_tab_ = (const uint16_t *)P(i_gelu);
+        exp_tab_ = (const uint16_t *)P(i_exp);
+    }
     word_ = mk_table(tw, m.word);
     type_ = mk_table(tt, m.ttype);
     pos_ = mk_table(tp, m.pos);
@@ -668,22 +684,22 @@ int Device::launch_all_f32(const int32_t *d_ids, const int32_t *d_cu, int n_seqs
     for (int l = 0; l < hp_.n_layer; ++l) {
         const DevLayer &L = layers_[(size_t)l];
         begin(K_GEMM_QKV, s, ev);
-        if (launch_f32_gemm(x32_, M, L.w32_qkv, 3 * d, d, L.b_qkv, 0, nullptr, qkv32_, s)) return -1;
+        if (launch_f32_gemm(x32_, M, L.w32_qkv, 3 * d, d, L.b_qkv, 0, nullptr, qkv32_, s, gelu_tab_)) return -1;
         end(K_GEMM_QKV, s, ev, 2.0 * t * 3.0 * d * d);
         begin(K_ATTENTION, s, ev);
-        if (launch_f32_attention(qkv32_, d_cu, n_seqs, max_len, hp_.n_head, d, att32_, s)) return -1;
+        if (launch_f32_attention(qkv32_, d_cu, n_seqs, max_len, hp_.n_head, d, att32_, s, exp_tab_)) return -1;
         end(K_ATTENTION, s, ev, att_flop_);
         begin(K_GEMM_O, s, ev);
-        if (launch_f32_gemm(att32_, M, L.w32_o, d, d, L.b_o, 2, x32_, z32_, s)) return -1;
+        if (launch_f32_gemm(att32_, M, L.w32_o, d, d, L.b_o, 2, x32_, z32_, s, gelu_tab_)) return -1;
         end(K_GEMM_O, s, ev, 2.0 * t * d * d);
         begin(K_LN_STATS, s, ev);
         launch_f32_ln(z32_, M, d, L.ln1_w, L.ln1_b, s);
         end(K_LN_STATS, s, ev, (double)M * d * 8.0);
         begin(K_GEMM_FFN_UP, s, ev);
-        if (launch_f32_gemm(z32_, M, L.w32_up, f, d, L.b_up, 1, nullptr, ffn32_, s)) return -1;
+        if (launch_f32_gemm(z32_, M, L.w32_up, f, d, L.b_up, 1, nullptr, ffn32_, s, gelu_tab_)) return -1;
         end(K_GEMM_FFN_UP, s, ev, 2.0 * t * d * f);
         begin(K_GEMM_FFN_DOWN, s, ev);
-        if (launch_f32_gemm(ffn32_, M, L.w32_down, d, f, L.b_down, 2, z32_, x32_, s)) return -1;
+        if (launch_f32_gemm(ffn32_, M, L.w32_down, d, f, L.b_down, 2, z32_, x32_, s, gelu_tab_)) return -1;
         end(K_GEMM_FFN_DOWN, s, ev, 2.0 * t * d * f);
         begin(K_LN_STATS, s, ev);
         launch_f32_ln(x32_, M, d, L.ln2_w, L.ln2_b, s);
@@ -855,6 +871,8 @@ extern "C" int32_t bertx_test_gemm_ln(int32_t fmt, int32_t N, int32_t K, const v
     return 0;
 }
 
+extern "C" int32_t bertx_test_gemm_ran(void) { return emb::g_gemm_ran; }
+
 // f32 chain GEMM (f32.hip) on host buffers: w f32 [N][K], x f32 [M][K], res/out f32 [M][N]
 extern "C" int32_t bertx_test_gemm_f32(int32_t N, int32_t K, const float *w, const float *bias, int32_t M,
                                        const float *x, int32_t epi, const float *res, float *out)
@@ -871,8 +889,11 @@ extern "C" int32_t bertx_test_gemm_f32(int32_t N, int32_t K, const float *w, con
     const float *dx = (const float *)B.up(x, (size_t)M * K * 4, (size_t)Mp * K * 4);
     const float *dr = epi == 2 ? (const float *)B.up(res, (size_t)M * N * 4, (size_t)Mp * N * 4) : nullptr;
     float *dout = (float *)B.up(nullptr, 0, (size_t)Mp * N * 4);
+    std::vector<uint16_t> tg, te;
+    era_tables(tg, te);
+    const uint16_t *dg = (const uint16_t *)B.up(tg.data(), tg.size() * 2, 0);
     if (B.bad) return -1;
-    if (launch_f32_gemm(dx, Mp, dw, N, K, db, epi, dr, dout, nullptr) != 0) return -1;
+    if (launch_f32_gemm(dx, Mp, dw, N, K, db, epi, dr, dout, nullptr, dg) != 0) return -1;
     HIP_RC(hipGetLastError());
     HIP_RC(hipDeviceSynchronize());
     HIP_RC(hipMemcpy(out, dout, (size_t)M * N * 4, hipMemcpyDeviceToHost));

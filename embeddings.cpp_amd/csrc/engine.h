@@ -100,9 +100,14 @@ public:
 
     const HParams &hp() const { return hp_; }
 
-    // the last bert_forward_batch / bert_encode_batch call's share of this replica
-    // (bertx_device_last_call): host wall time of its forwards, sentences, tokens
-    void set_last_call(double ms, int seqs, int64_t tokens) { lc_ms_ = ms; lc_seqs_ = seqs; lc_tokens_ = tokens; }
+    // the last bert_forward_batch / bert_encode_batch call that ran on this replica
+    // (bertx_device_last_call): host wall time of its forwards, sentences, tokens;
+    // calls() counts the host-driven calls that ran here (bertx_device_calls)
+    void set_last_call(double ms, int seqs, int64_t tokens)
+    {
+        lc_ms_ = ms; lc_seqs_ = seqs; lc_tokens_ = tokens; ++calls_;
+    }
+    int64_t calls() const { return calls_; }
     double last_call_ms() const { return lc_ms_; }
     int last_call_seqs() const { return lc_seqs_; }
     int64_t last_call_tokens() const { return lc_tokens_; }
@@ -149,6 +154,7 @@ private:
     std::vector<DevLayer> layers_;
     int wfmt_ = FMT_F16;
     bool f32_ = false;              // ftype 0 file: the f32 chain (f32.hip)
+    const uint16_t *gelu_tab_ = nullptr, *exp_tab_ = nullptr;   // f32 chain: the era's fp16 tables (host-built)
 
     // workspace
     int64_t cap_tokens_ = 0, cap_seqs_ = 0, cap_pool_ = 0;   // cap_pool_: pool partial rows (seqs x chunks)
@@ -177,6 +183,7 @@ private:
     double lc_ms_ = 0.0;
     int lc_seqs_ = 0;
     int64_t lc_tokens_ = 0;
+    int64_t calls_ = 0;
 
     bool profiling_ = false;
     double att_flop_ = 0.0;         // attention FLOP of the forward being launched

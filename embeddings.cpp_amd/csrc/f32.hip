@@ -14,6 +14,7 @@
 #include "kernels.h"
 #include "table_read.h"
 
+#include <atomic>
 #include <cmath>
 
 namespace emb {
@@ -59,8 +60,10 @@ __device__ __forceinline__ void ln_row(f32x4 (&v)[F32_MAXC], int d, int lane, co
         const int c = 4 * lane + 256 * k;
         if (c < d) {
             const f32x4 gg = *(const f32x4 *)(g + c), bb = *(const f32x4 *)(b + c);
+            // ggml_norm's y = c * scale, then ggml_mul (gamma) and ggml_add (beta):
+            // three rounded ops, no contraction (bert.cpp:977-984, 1051-1055)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[k][e] = fmaf(gg[e], v[k][e] * scale, bb[e]);
+            for (int e = 0; e < 4; ++e) v[k][e] = __fadd_rn(__fmul_rn(gg[e], __fmul_rn(v[k][e], scale)), bb[e]);
         }
     }
 }
@@ -117,26 +120,27 @@ __global__ __launch_bounds__(256) void f32_ln_kernel(float *__restrict__ x, int 
 
 // ---------------------------------------------------------------- GEMM
 
-// The era's fp16-table GELU: gelu(f16(x)) rounded to f16 (oracle/ggml_era.c tables).
-__device__ __forceinline__ float gelu_table(float v)
+// The era's fp16 tables (GELU, exp), built on the host with libm at load
+// (model_file.cpp era_tables) and indexed by the f16 bit pattern of the input:
+// T(f16(x)), bit for bit the table ggml held.
+__device__ __forceinline__ float era_table(const uint16_t *__restrict__ tab, float v)
 {
-    const float f = (float)(h16)v;
-    const float g = 0.5f * f * (1.0f + tanhf(0.79788456080286535587989211986876f * f * (1.0f + 0.044715f * f * f)));
-    return (float)(h16)g;
+    return (float)as_h(tab[__builtin_bit_cast(uint16_t, (h16)v)]);
 }
 
 // Y[m][n] = epi(sum_k X[m][k] W[n][k]) on 64 x 64 tiles, 4 waves of 32 x 32
 // (2 x 2 v_mfma_f32_16x16x4_f32 tiles each), K in steps of 32 through
 // LDS (rows padded to 33 floats).  A = X (lane: row l & 15, k = l >> 4), B = W^T
 // (k = l >> 4, feature l & 15); D lane: feature l & 15, tokens 4 (l >> 4) + r.
-// EPI: 0 bias + acc, 1 gelu_table(bias + acc), 2 (bias + acc) + res (the
+// EPI: 0 bias + acc, 1 GELU table(bias + acc), 2 (bias + acc) + res (the
 // reference's operand order, bert.cpp:1040-1045, 1066-1072).
 constexpr int F32_BK = 32;
 
 template <int EPI>
 __global__ __launch_bounds__(256) void f32_gemm_kernel(const float *__restrict__ X, const float *__restrict__ W,
                                                        const float *__restrict__ bias, const float *__restrict__ res,
-                                                       float *__restrict__ Y, int N, int K, int nN)
+                                                       float *__restrict__ Y, int N, int K, int nN,
+                                                       const uint16_t *__restrict__ gelu_tab)
 {
     __shared__ float xs[64][F32_BK + 1], ws[64][F32_BK + 1];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -187,7 +191,7 @@ __global__ __launch_bounds__(256) void f32_gemm_kernel(const float *__restrict__
             for (int r = 0; r < 4; ++r) {
                 const size_t o = (size_t)(m0 + wm + 16 * i + 4 * (lane >> 4) + r) * N + n;
                 float v = bv + acc[i][j][r];
-                if (EPI == 1) v = gelu_table(v);
+                if (EPI == 1) v = era_table(gelu_tab, v);
                 if (EPI == 2) v = v + res[o];
                 Y[o] = v;
             }
@@ -204,7 +208,8 @@ __global__ __launch_bounds__(256) void f32_gemm_kernel(const float *__restrict__
 // (packed sentences); the reference's mask makes theirs contribute exactly 0.
 template <int DH>
 __global__ __launch_bounds__(256) void f32_attention_kernel(const float *__restrict__ qkv, const int32_t *__restrict__ cu,
-                                                            int d, int s_stride, float scale, float *__restrict__ out)
+                                                            int d, int s_stride, float scale, float *__restrict__ out,
+                                                            const uint16_t *__restrict__ exp_tab)
 {
     extern __shared__ float smem[];
     float(*qs)[DH] = (float(*)[DH])smem;                      // [16][DH]
@@ -243,7 +248,7 @@ __global__ __launch_bounds__(256) void f32_attention_kernel(const float *__restr
     for (int o = 8; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
     double sum = 0.0;
     for (int k = l16; k < len; k += 16) {
-        const float e = (float)(h16)expf((float)(h16)(row[k] - mx));
+        const float e = era_table(exp_tab, row[k] - mx);
         row[k] = e;
         sum += (double)e;
     }
@@ -322,27 +327,49 @@ void launch_f32_ln(float *x, int32_t rows, int32_t d, const float *g, const floa
 }
 
 int launch_f32_gemm(const float *X, int32_t M, const float *W, int32_t N, int32_t K, const float *bias, int32_t epi,
-                    const float *res, float *Y, hipStream_t s)
+                    const float *res, float *Y, hipStream_t s, const uint16_t *gelu_tab)
 {
-    if (M % 64 || K % F32_BK || N <= 0 || M <= 0 || epi < 0 || epi > 2 || (epi == 2 && !res)) return -1;
+    if (M % 64 || K % F32_BK || N <= 0 || M <= 0 || epi < 0 || epi > 2 || (epi == 2 && !res) ||
+        (epi == 1 && !gelu_tab))
+        return -1;
     const int nN = (N + 63) / 64, grid = (M / 64) * nN;
-    if (epi == 0) f32_gemm_kernel<0><<<grid, 256, 0, s>>>(X, W, bias, res, Y, N, K, nN);
-    else if (epi == 1) f32_gemm_kernel<1><<<grid, 256, 0, s>>>(X, W, bias, res, Y, N, K, nN);
-    else f32_gemm_kernel<2><<<grid, 256, 0, s>>>(X, W, bias, res, Y, N, K, nN);
+    if (epi == 0) f32_gemm_kernel<0><<<grid, 256, 0, s>>>(X, W, bias, res, Y, N, K, nN, gelu_tab);
+    else if (epi == 1) f32_gemm_kernel<1><<<grid, 256, 0, s>>>(X, W, bias, res, Y, N, K, nN, gelu_tab);
+    else f32_gemm_kernel<2><<<grid, 256, 0, s>>>(X, W, bias, res, Y, N, K, nN, gelu_tab);
     return 0;
 }
 
+// Largest dynamic LDS one workgroup may request on the calling thread's device
+// (cached per ordinal; gfx950: 160 KiB).
+static size_t device_lds_limit()
+{
+    static std::atomic<int> cache[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0) { (void)hipGetLastError(); return 65536; }
+    if (dev < 64 && cache[dev].load(std::memory_order_relaxed) > 0) return (size_t)cache[dev].load(std::memory_order_relaxed);
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess || n <= 0) {
+        (void)hipGetLastError();
+        n = 65536;
+    }
+    if (dev < 64) cache[dev].store(n, std::memory_order_relaxed);
+    return (size_t)n;
+}
+
 int launch_f32_attention(const float *qkv, const int32_t *cu, int32_t n_seqs, int32_t max_len, int32_t n_head,
-                         int32_t d, float *out, hipStream_t s)
+                         int32_t d, float *out, hipStream_t s, const uint16_t *exp_tab)
 {
     const int dh = d / n_head;
-    if (d % n_head || (dh != 32 && dh != 64) || max_len <= 0 || max_len > 2048) return -1;
+    if (d % n_head || (dh != 32 && dh != 64) || max_len <= 0 || !exp_tab) return -1;
     const int s_stride = (max_len + 3) / 4 * 4;
     const size_t lds = sizeof(float) * (16 * (size_t)dh + 64 * (size_t)(dh + 1) + 16 * (size_t)s_stride);
+    // the 16 score rows live in LDS: refuse (before launching anything) a length
+    // whose rows do not fit the device's per-workgroup LDS
+    if (lds > device_lds_limit()) return -1;
     const dim3 g((max_len + 15) / 16, n_head, n_seqs);
     const float scale = 1.0f / sqrtf((float)dh);
-    if (dh == 64) f32_attention_kernel<64><<<g, 256, lds, s>>>(qkv, cu, d, s_stride, scale, out);
-    else f32_attention_kernel<32><<<g, 256, lds, s>>>(qkv, cu, d, s_stride, scale, out);
+    if (dh == 64) f32_attention_kernel<64><<<g, 256, lds, s>>>(qkv, cu, d, s_stride, scale, out, exp_tab);
+    else f32_attention_kernel<32><<<g, 256, lds, s>>>(qkv, cu, d, s_stride, scale, out, exp_tab);
     return 0;
 }
 

@@ -529,7 +529,14 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     // with them behind X(ks + 1) -- left the last LQ pieces of X(ks + 1) in flight
     // across the barrier: the NS 2 ring at KS % 3 == 2, the 4-set ring at
     // KS % 4 == 2.  The tail now issues ztail_dma pieces in their place.)
+    // Both counters drained in front of the epilogue: the K loop's B-fragment reads
+    // are asm (zds_read) with hand-counted lgkmcnt waits the compiler cannot see, so
+    // without an explicit lgkmcnt(0) here an asm read still in flight could land in
+    // a register hipcc hands to the epilogue (round 3's pipelined private-ring
+    // variant faulted exactly so; scripts/check_drain.py checks the
+    // shipped code objects for this wait).
     wait_vmcnt<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     ZSTAMP(2, __builtin_amdgcn_s_memtime());
 #ifdef GEMM_STAMPS
     ZSTAMP(4, __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11)));
@@ -731,9 +738,18 @@ void dispatch_z(const DevWeight &W, const h16 *x, int M, const float *bias, int 
     }
 }
 
+// The shipped tile configs (round 4 pruned the A/B zoo to these; every config
+// computes each output with the same MFMA sequence, so all give the same bits):
+//   2   4 waves 256 x 128, X pieces among the MFMAs   large batches (production)
+//   11  4 waves 256 x 128, X pieces in one burst       the large regime's A/B form
+//   3   4 waves 128 x 128                              one tile per CU
+//   4   2 waves 64 x 64                                small batches, >= half the CUs
+//   16  4 waves 64 x 64, 2 along the tokens, wave-private X rings
+//                                                      small batches, < half the CUs
+// A config whose row tile does not divide M falls back to the next smaller tile.
 template <int FMT>
-void launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, int32_t epi, const void *res,
-                void *out, hipStream_t s, LnFold ln, bool lnf, int cfg)
+int launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, int32_t epi, const void *res,
+               void *out, hipStream_t s, LnFold ln, bool lnf, int cfg)
 {
     if (cfg == 0) {
         // the largest tile that still gives every CU work: 256 x 128 tiles two per CU
@@ -745,17 +761,14 @@ void launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, 
         // half as long; B = 1, L = 32: 632 -> 571 us) with wave-private X rings (no
         // barrier in the K loop: 582 -> 567 us, profiles/r03_gemm_private_ab.log),
         // else on 2 (C2's O-proj and FFN-down: the 4-wave forms 6-15 % slower
-        // there).  Same bits either way.  BERT_GEMM_SMALL = 4 / 7 / 8 / 16 / 17
-        // forces one form (8: 64 x 32 on 2 waves; 17: 4 with private rings).
-        static const int small_env = [] { const char *e = std::getenv("BERT_GEMM_SMALL"); return e ? std::atoi(e) : 0; }();
+        // there).  Same bits either way.
         const long n64 = (long)(M / 64) * ((W.N + 63) / 64);
-        const int small = (small_env == 4 || small_env == 7 || small_env == 8 || small_env == 16 || small_env == 17) ? small_env : (2 * n64 < cus ? 16 : 4);
+        const int small = 2 * n64 < cus ? 16 : 4;
         cfg = (M % 256 == 0 && (M / 256) * n128 >= 2 * cus) ? 2 : (M % 128 == 0 && (M / 128) * n128 >= cus) ? 3 : small;
-        // BERT_GEMM_XI = 1: the 128- and 64-row forms with the X pieces among the
-        // MFMAs too (cfg 13 / 14 / 15; A/B)
-        static const bool xi_env = [] { const char *e = std::getenv("BERT_GEMM_XI"); return e && *e == '1'; }();
-        if (xi_env) cfg = cfg == 3 ? 13 : cfg == 4 ? 14 : cfg == 7 ? 15 : cfg;
     }
+    if ((cfg == 2 || cfg == 11) && M % 256) cfg = 3;
+    if (cfg == 3 && M % 128) cfg = 4;
+    if (cfg != 2 && cfg != 11 && cfg != 3 && cfg != 16) cfg = 4;
     // Non-temporal output stores on the 256-row tiles (large batches): the output
     // streams past L2 instead of evicting the X panels the next column tiles read
     // (C3: FFN-down 143 -> 140 us, QKV -1 us, forward +0.5 % alternating on one box,
@@ -767,24 +780,20 @@ void launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, 
     // 256 x 128: the X pieces among the MFMAs (one per B-fragment item from the
     // K-step's start; +1.2-1.6 % on the C3 forward over one burst in front of them,
     // profiles/r03_gemm_xi_ab.log); cfg 11 keeps the burst form for A/B
-    if (cfg == 2 && M % 256 == 0) dispatch_z<FMT, 4, 256, 2, 1, 3, 1, 2>(W, x, M, bias, epi, res, out, s, ln, lnf);
-    else if (cfg == 11 && M % 256 == 0) dispatch_z<FMT, 4, 256, 2>(W, x, M, bias, epi, res, out, s, ln, lnf);
-    else if (cfg == 13 && M % 128 == 0) dispatch_z<FMT, 4, 128, 4, 1, 3, 1, 2>(W, x, M, bias, epi, res, out, s, ln, lnf);
-    else if (cfg == 14 && M % 64 == 0) dispatch_z<FMT, 2, 64, 4, 1, 3, 1, 2>(W, x, M, bias, epi, res, out, s, ln, lnf);
-    else if (cfg == 15 && M % 64 == 0) dispatch_z<FMT, 4, 64, 4, 1, 3, 2, 2>(W, x, M, bias, epi, res, out, s, ln, lnf);
-    else if (cfg == 16 && M % 64 == 0) dispatch_z<FMT, 4, 64, 4, 1, 3, 2, 3>(W, x, M, bias, epi, res, out, s, ln, lnf);
-    else if (cfg == 17 && M % 64 == 0) dispatch_z<FMT, 2, 64, 4, 1, 3, 1, 3>(W, x, M, bias, epi, res, out, s, ln, lnf);
-    else if (cfg == 5 && M % 128 == 0) dispatch_z<FMT, 4, 128, 4, 2>(W, x, M, bias, epi, res, out, s, ln, lnf);
-    else if (cfg != 4 && M % 128 == 0) dispatch_z<FMT, 4, 128, 4>(W, x, M, bias, epi, res, out, s, ln, lnf);
-    else if (cfg == 6 && M % 64 == 0) dispatch_z<FMT, 2, 64, 4, 1, 4>(W, x, M, bias, epi, res, out, s, ln, lnf);
-    else if (cfg == 7 && M % 64 == 0) dispatch_z<FMT, 4, 64, 4, 1, 3, 2>(W, x, M, bias, epi, res, out, s, ln, lnf);
-    else if (cfg == 8 && M % 64 == 0) dispatch_z<FMT, 2, 64, 4, 1, 3, 2>(W, x, M, bias, epi, res, out, s, ln, lnf);
-    else dispatch_z<FMT, 2, 64, 4>(W, x, M, bias, epi, res, out, s, ln, lnf);
+    switch (cfg) {
+    case 2: dispatch_z<FMT, 4, 256, 2, 1, 3, 1, 2>(W, x, M, bias, epi, res, out, s, ln, lnf); break;
+    case 11: dispatch_z<FMT, 4, 256, 2>(W, x, M, bias, epi, res, out, s, ln, lnf); break;
+    case 3: dispatch_z<FMT, 4, 128, 4>(W, x, M, bias, epi, res, out, s, ln, lnf); break;
+    case 16: dispatch_z<FMT, 4, 64, 4, 1, 3, 2, 3>(W, x, M, bias, epi, res, out, s, ln, lnf); break;
+    default: dispatch_z<FMT, 2, 64, 4>(W, x, M, bias, epi, res, out, s, ln, lnf); break;
+    }
+    return cfg;
 }
 
 }  // namespace
 
 thread_local int g_gemm_cfg = 0;
+thread_local int g_gemm_ran = 0;
 
 // CUs of the calling thread's current device, cached per ordinal (a context may
 // hold devices in different partition modes; launches size persistent grids
@@ -830,10 +839,10 @@ int launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *b
     static const int env_cfg = [] { const char *e = std::getenv("BERT_GEMM_CFG"); return e ? std::atoi(e) : 0; }();
     const int cfg = g_gemm_cfg ? g_gemm_cfg : env_cfg;
     switch (W.fmt) {
-    case FMT_Q4_0: launch_fmt<FMT_Q4_0>(W, x, M, bias, epi, res, out, s, lnx, lnf, cfg); break;
-    case FMT_Q4_1: launch_fmt<FMT_Q4_1>(W, x, M, bias, epi, res, out, s, lnx, lnf, cfg); break;
-    case FMT_Q8_0: launch_fmt<FMT_Q8_0>(W, x, M, bias, epi, res, out, s, lnx, lnf, cfg); break;
-    default: launch_fmt<FMT_F16>(W, x, M, bias, epi, res, out, s, lnx, lnf, cfg); break;
+    case FMT_Q4_0: g_gemm_ran = launch_fmt<FMT_Q4_0>(W, x, M, bias, epi, res, out, s, lnx, lnf, cfg); break;
+    case FMT_Q4_1: g_gemm_ran = launch_fmt<FMT_Q4_1>(W, x, M, bias, epi, res, out, s, lnx, lnf, cfg); break;
+    case FMT_Q8_0: g_gemm_ran = launch_fmt<FMT_Q8_0>(W, x, M, bias, epi, res, out, s, lnx, lnf, cfg); break;
+    default: g_gemm_ran = launch_fmt<FMT_F16>(W, x, M, bias, epi, res, out, s, lnx, lnf, cfg); break;
     }
     return 0;
 }

@@ -35,6 +35,8 @@ inline size_t fmt_row_bytes(int f, int64_t k) { return fmt_block_bytes(f) * (siz
 // astype(float16) in convert-to-ggml.py and F16C use).
 uint16_t f32_to_f16(float f);
 float f16_to_f32(uint16_t h);
+// The era's 65536-entry fp16 GELU and exp tables (model_file.cpp).
+void era_tables(std::vector<uint16_t> &gelu, std::vector<uint16_t> &ex);
 
 struct HParams {
     int32_t n_vocab = 0, n_max_tokens = 0, n_embd = 0, n_intermediate = 0, n_head = 0, n_layer = 0, ftype = 0;

@@ -93,10 +93,12 @@ struct LnFold {
 // element-wise).  Returns 0, or -1 for an unsupported shape.
 int launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi,
                 const void *res, void *out, hipStream_t s, const LnFold &ln = LnFold());
-// Tests/benches: tile config (0 = heuristic, 2 = 4 waves 256x128, 3 = 4 waves 128x128,
-// 4 = 2 waves 64x64, 5 = 4 waves 128x256, 6 = 64x64 with the 4-set weight ring).
-// Per calling thread, so a test hook never changes a forward running on another thread.
+// Tests/benches: tile config (0 = heuristic; the shipped configs are listed at
+// gemm.hip launch_fmt: 2, 11, 3, 4, 16).  Per calling thread, so a test hook never
+// changes a forward running on another thread.  g_gemm_ran: the config the
+// calling thread's last launch_gemm actually dispatched (after fallbacks).
 extern thread_local int g_gemm_cfg;
+extern thread_local int g_gemm_ran;
 
 // CU count of the calling thread's current HIP device (cached per ordinal).
 int device_cu_count();
@@ -134,14 +136,16 @@ void launch_f32_embed_ln(const DevTable &word, const DevTable &type, const DevTa
                          int32_t d, float *x, hipStream_t s);
 // In-place LayerNorm of rows [0, rows) (ggml_norm, f64 sums, eps 1e-5).
 void launch_f32_ln(float *x, int32_t rows, int32_t d, const float *g, const float *b, hipStream_t s);
-// Y[M][N] = epi(X[M][K] W[N][K]^T): 0 bias + acc, 1 era GELU(bias + acc), 2 (bias + acc)
-// + res.  M % 64 == 0, K % 32 == 0; returns -1 otherwise.
+// Y[M][N] = epi(X[M][K] W[N][K]^T): 0 bias + acc, 1 era GELU(bias + acc) through the
+// f16-indexed table gelu_tab [65536] (host_common.h era_tables, uploaded to the
+// device), 2 (bias + acc) + res.  M % 64 == 0, K % 32 == 0; returns -1 otherwise.
 int launch_f32_gemm(const float *X, int32_t M, const float *W, int32_t N, int32_t K, const float *bias, int32_t epi,
-                    const float *res, float *Y, hipStream_t s);
-// Per (sentence, head) softmax(Q K^T / sqrt(dh)) V with the era's fp16-table exp,
-// qkv f32 [T][3d] -> out f32 [T][d]; dh 32 or 64, max_len <= 2048, else -1.
+                    const float *res, float *Y, hipStream_t s, const uint16_t *gelu_tab);
+// Per (sentence, head) softmax(Q K^T / sqrt(dh)) V with the era's fp16-table exp
+// (exp_tab [65536] on the device), qkv f32 [T][3d] -> out f32 [T][d]; dh 32 or 64
+// and the 16 score rows of max_len keys within the device's LDS, else -1.
 int launch_f32_attention(const float *qkv, const int32_t *cu, int32_t n_seqs, int32_t max_len, int32_t n_head,
-                         int32_t d, float *out, hipStream_t s);
+                         int32_t d, float *out, hipStream_t s, const uint16_t *exp_tab);
 // out[b] = mean_{i<len} x[start + i] / ||.|| (bert.cpp:1087-1095).
 void launch_f32_pool(const float *x, const int32_t *cu, int32_t n_seqs, int32_t d, float *out, hipStream_t s);
 

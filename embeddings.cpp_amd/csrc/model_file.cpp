@@ -57,6 +57,23 @@ float f16_to_f32(uint16_t h)
     return f;
 }
 
+// The ggml-era fp16 function tables bert.cpp's GELU and softmax exp read
+// (GGML_GELU_FP16 / the fp16 exp table, bert.cpp:1025, 1063): entry i = f16 of the
+// f32 function at the f16 value i, built once on the host with libm, as ggml did
+// at ggml_init.  The f32 chain (f32.hip) indexes them by the f16 bit pattern.
+void era_tables(std::vector<uint16_t> &gelu, std::vector<uint16_t> &ex)
+{
+    gelu.resize(65536);
+    ex.resize(65536);
+    const float k_a = 0.044715f, k_s = 0.79788456080286535587989211986876f;   // sqrt(2/pi)
+    for (uint32_t i = 0; i < 65536u; ++i) {
+        const float f = f16_to_f32((uint16_t)i);
+        const float g = 0.5f * f * (1.0f + std::tanh(k_s * f * (1.0f + k_a * f * f)));
+        gelu[i] = f32_to_f16(g);
+        ex[i] = f32_to_f16(std::exp(f));
+    }
+}
+
 void dequant_row(int fmt, const uint8_t *src, float *dst, int64_t k)
 {
     const int64_t nb = k / QK;

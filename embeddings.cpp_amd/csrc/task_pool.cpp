@@ -1,6 +1,7 @@
 #include "task_pool.h"
 
 #include <algorithm>
+#include <pthread.h>
 
 namespace emb {
 
@@ -8,6 +9,36 @@ TaskPool &TaskPool::instance()
 {
     static TaskPool pool;
     return pool;
+}
+
+TaskPool::TaskPool()
+{
+    // fork safety: no batch may be in flight across a fork (prepare takes both
+    // locks, so a fork waits for a running batch); the child has none of the
+    // parent's workers, so it drops their handles (leaked on purpose: joining or
+    // destroying a std::thread of another process is undefined) and starts its
+    // own on demand
+    pthread_atfork([] { instance().before_fork(); }, [] { instance().after_fork(false); },
+                   [] { instance().after_fork(true); });
+}
+
+void TaskPool::before_fork()
+{
+    run_mu_.lock();
+    mu_.lock();
+}
+
+void TaskPool::after_fork(bool child)
+{
+    if (child) {
+        if (!threads_.empty()) new std::vector<std::thread>(std::move(threads_));   // never joined, never freed
+        threads_.clear();
+        active_ = busy_ = 0;
+        fn_ = nullptr;
+        error_ = nullptr;
+    }
+    mu_.unlock();
+    run_mu_.unlock();
 }
 
 TaskPool::~TaskPool()
@@ -33,7 +64,15 @@ void TaskPool::drain()
     for (;;) {
         const int64_t i = next_.fetch_add(1, std::memory_order_relaxed);
         if (i >= n_tasks_) return;
-        (*fn_)(i);
+        try {
+            (*fn_)(i);
+        } catch (...) {
+            // the first exception of the batch is kept for run() to rethrow; the
+            // remaining tasks are abandoned (no thread dies with it)
+            std::lock_guard<std::mutex> lk(mu_);
+            if (!error_) error_ = std::current_exception();
+            next_.store(n_tasks_, std::memory_order_relaxed);
+        }
     }
 }
 
@@ -72,14 +111,21 @@ void TaskPool::run(int64_t n_tasks, int n_threads, const std::function<void(int6
         next_.store(0, std::memory_order_relaxed);
         active_ = helpers;
         busy_ = helpers;
+        error_ = nullptr;
         ++gen_;
     }
     cv_work_.notify_all();
     drain();
-    std::unique_lock<std::mutex> lk(mu_);
-    cv_done_.wait(lk, [&] { return busy_ == 0; });
-    active_ = 0;
-    fn_ = nullptr;
+    std::exception_ptr err;
+    {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_done_.wait(lk, [&] { return busy_ == 0; });
+        active_ = 0;
+        fn_ = nullptr;
+        err = error_;
+        error_ = nullptr;
+    }
+    if (err) std::rethrow_exception(err);
 }
 
 }  // namespace emb

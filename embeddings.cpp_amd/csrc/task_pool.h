@@ -3,12 +3,15 @@
 // and parked on a condition variable between batches, so a call costs a wake-up
 // instead of n thread creations; tasks are claimed dynamically (an atomic
 // counter), the calling thread works too, and run() returns when every task is
-// done.  One batch at a time: concurrent callers queue on the pool's mutex.
+// done.  One batch at a time: concurrent callers queue on the pool's mutex.  A
+// task that throws ends the batch and run() rethrows the first exception in the
+// caller; a forked child gets a fresh pool (pthread_atfork).
 #pragma once
 
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
+#include <exception>
 #include <functional>
 #include <mutex>
 #include <thread>
@@ -22,13 +25,15 @@ public:
     ~TaskPool();
 
     // fn(i) for every i in [0, n_tasks) on up to n_threads threads (the caller
-    // included); blocks until all are done.
+    // included); blocks until all are done, then rethrows a task's exception.
     void run(int64_t n_tasks, int n_threads, const std::function<void(int64_t)> &fn);
 
     static constexpr int kMaxThreads = 256;
 
 private:
-    TaskPool() = default;
+    TaskPool();
+    void before_fork();
+    void after_fork(bool child);
     void grow(int n_workers);
     void worker(int idx);
     void drain();
@@ -44,6 +49,7 @@ private:
     int busy_ = 0;                         // enlisted workers not yet finished
     uint64_t gen_ = 0;                     // batch generation (wakes parked workers)
     bool stop_ = false;
+    std::exception_ptr error_;             // first exception thrown by a task of the batch
 };
 
 }  // namespace emb

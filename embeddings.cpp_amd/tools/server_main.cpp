@@ -10,15 +10,21 @@
 // The serving model differs.  The reference accepts one client at a time
 // (listen backlog 1) and runs one bert_encode per recv.  Here every connection
 // has its own thread, which tokenizes its text (bert_tokenize, host) and queues
-// it; one batcher thread sends the queued texts (at most --max-batch) to the GPU
-// as ONE bert_forward_batch as soon as every connected client has a text queued,
-// or --wait-us after the first one arrived, whichever comes first (so a lone
-// client never waits for a batch that cannot fill).  Per-sentence results do not depend on the batch they ride
-// in (tests/test_gpu_forward.py batch invariance), so every reply equals the
-// single-text result.
+// it; one batcher thread per GPU replica of the context (bertx_num_devices) takes
+// queued texts (at most --max-batch) and sends them to the GPUs as ONE
+// bert_forward_batch, so each replica can have a micro-batch in flight (the
+// library routes a micro-batch whole to its least-loaded replica, bert_abi.cpp
+// run_forward).  A batcher's window opens with the first queued text and closes
+// when the clients that are not already waiting on an in-flight batch have queued
+// their share of the free batchers (ceil(waiting clients / free batchers)), or
+// --wait-us after it opened, whichever comes first (so a lone client never waits
+// for a batch that cannot fill).  Per-sentence results do not depend on the batch
+// they ride in (tests/test_gpu_forward.py batch invariance), so every reply equals
+// the single-text result.
 //
 // usage: server -m MODEL [--port P] [-t N] [--max-batch B] [--wait-us U]
 #include "bert.h"
+#include "bert_hip.h"
 
 #include <arpa/inet.h>
 #include <netinet/in.h>
@@ -32,6 +38,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <deque>
 #include <mutex>
 #include <string>
@@ -49,8 +56,8 @@ struct Request {
 
 class Batcher {
 public:
-    Batcher(bert_ctx *ctx, int n_threads, int max_batch, int wait_us)
-        : ctx_(ctx), n_threads_(n_threads), max_batch_(max_batch), wait_us_(wait_us)
+    Batcher(bert_ctx *ctx, int n_threads, int max_batch, int wait_us, int n_batchers)
+        : ctx_(ctx), n_threads_(n_threads), max_batch_(max_batch), wait_us_(wait_us), n_batchers_(n_batchers)
     {
     }
 
@@ -84,15 +91,21 @@ public:
                 std::unique_lock<std::mutex> lk(mu_);
                 cv_in_.wait(lk, [&] { return !queue_.empty(); });
                 // the window opens with the first queued text and closes early once
-                // every connected client has a text queued
+                // the clients not waiting on an in-flight batch have queued this
+                // batcher's share of them
                 cv_in_.wait_for(lk, std::chrono::microseconds(wait_us_), [&] {
-                    const int full = clients_ < max_batch_ ? (clients_ > 1 ? clients_ : 1) : max_batch_;
+                    const int waiting = std::max(1, clients_ - in_flight_);
+                    const int free = std::max(1, n_batchers_ - busy_);
+                    const int full = std::min(max_batch_, (waiting + free - 1) / free);
                     return (int)queue_.size() >= full;
                 });
                 while (!queue_.empty() && (int)batch.size() < max_batch_) {
                     batch.push_back(queue_.front());
                     queue_.pop_front();
                 }
+                if (batch.empty()) continue;   // another batcher took them
+                ++busy_;
+                in_flight_ += (int)batch.size();
             }
             toks.clear();
             lens.clear();
@@ -106,15 +119,20 @@ public:
             {
                 std::lock_guard<std::mutex> g(mu_);
                 for (Request *r : batch) r->done = true;
+                --busy_;
+                in_flight_ -= (int)batch.size();
             }
             cv_out_.notify_all();
+            cv_in_.notify_all();   // a waiting batcher's share changed
         }
     }
 
 private:
     bert_ctx *ctx_;
-    int n_threads_, max_batch_, wait_us_;
+    int n_threads_, max_batch_, wait_us_, n_batchers_;
     int clients_ = 0;
+    int busy_ = 0;        // batchers with a micro-batch on the GPUs
+    int in_flight_ = 0;   // texts in those micro-batches
     std::mutex mu_;
     std::condition_variable cv_in_, cv_out_;
     std::deque<Request *> queue_;
@@ -192,11 +210,13 @@ int main(int argc, char **argv)
         std::perror("bind/listen");
         return 1;
     }
-    std::printf("Server running on port %d: up to %d texts per GPU batch, %d us window\n", params.port, max_batch,
-                wait_us);
+    std::printf("Server running on port %d: up to %d texts per GPU batch, %d us window, %d batcher(s)\n", params.port,
+                max_batch, wait_us, std::max(1, (int)bertx_num_devices(ctx)));
     std::fflush(stdout);
-    Batcher batcher(ctx, params.n_threads, max_batch, wait_us);
-    std::thread(&Batcher::loop, &batcher).detach();
+    // one batcher (one micro-batch in flight) per GPU replica of the context
+    const int n_batchers = std::max(1, (int)bertx_num_devices(ctx));
+    Batcher batcher(ctx, params.n_threads, max_batch, wait_us, n_batchers);
+    for (int i = 0; i < n_batchers; ++i) std::thread(&Batcher::loop, &batcher).detach();
     for (;;) {
         const int fd = accept(srv, nullptr, nullptr);
         if (fd < 0) {

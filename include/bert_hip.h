@@ -55,14 +55,24 @@ BERT_API int32_t bertx_kernel_stats(struct bert_ctx *ctx, int32_t idx, const cha
                                     int32_t *work_is_flops);
 
 /*
- * Multi-GPU balance of the last host-driven call (bert_forward_batch /
- * bert_encode_batch, which shard sentences over the context's GPUs by FLOP cost,
- * reference entry point bert.cpp:1374-1444): GPU `slot`'s host wall time for its
- * share (staging, H2D, forward, D2H), its sentence and token counts.  Returns 0,
- * or -1 for a bad slot.
+ * Multi-GPU balance of the last host-driven call that ran on GPU `slot`
+ * (bert_forward_batch / bert_encode_batch, which route or shard sentences over the
+ * context's GPUs by FLOP cost, reference entry point bert.cpp:1374-1444): its host
+ * wall time for its share (staging, H2D, forward, D2H), its sentence and token
+ * counts.  Returns 0, or -1 for a bad slot.
  */
 BERT_API int32_t bertx_device_last_call(struct bert_ctx *ctx, int32_t slot, double *wall_ms, int32_t *n_seqs,
                                         int64_t *n_tokens);
+
+/*
+ * Number of host-driven calls (bert_forward_batch / bert_encode_batch shares) that
+ * have run on replica `slot` since load, or -1 for a bad slot.  Routing rule of
+ * those calls (bert_abi.cpp run_forward): a call of T tokens uses
+ * k = clamp(T / 8192, 1, replicas) replicas, the k least-loaded by the work still in
+ * flight on them (ties rotate), split by cost; so concurrent small calls land on
+ * different replicas and a large batch spreads over all of them.
+ */
+BERT_API int64_t bertx_device_calls(struct bert_ctx *ctx, int32_t slot);
 
 /* Native quantizer (mirrors models/quantize.cpp): f32/f16 file -> itype
  * 2 (q4_0), 3 (q4_1) or 8 (q8_0, extension).  Returns 0 on success. */
@@ -81,9 +91,10 @@ BERT_API int32_t bertx_convert_hf(const char *dir_model, const char *fname_out, 
  * in format `fmt` = 0,1,2,3,8).  x: f16 bits [M][K].  epi: 0 = +bias -> f16,
  * 1 = +bias, era GELU -> f16, 2 = +bias +res -> f16 (res f16 [M][N], the
  * residual-stream form; sum in f32, computed in place over res).  cfg: GEMM tile
- * config (0 = the production heuristic, 2 = 4 waves 256x128, 3 = 4 waves 128x128,
- * 4 = 2 waves 64x64, 5 = 4 waves 128x256, 6 = 2 waves 64x64 with a 4-set weight
- * register ring).
+ * config (0 = the production heuristic, 2 = 4 waves 256x128, 11 = the same with
+ * the X pieces in one burst, 3 = 4 waves 128x128, 4 = 2 waves 64x64, 16 = 4 waves
+ * 64x64 with wave-private X rings); a tile that does not divide the padded M falls
+ * back to the next smaller one — bertx_test_gemm_ran() reports what ran.
  * Reference interface these kernels replace: ggml_mul_mat + ggml_add (+ ggml_gelu)
  * at bert.cpp:994-1016, 1040-1045, 1059-1072.
  */
@@ -108,6 +119,10 @@ BERT_API int32_t bertx_test_gemm_ln(int32_t fmt, int32_t N, int32_t K, const voi
                                     const float *in_b, int32_t epi, const uint16_t *res, const float *res_stats,
                                     const float *res_g, const float *res_b, const float *g_next, uint16_t *out,
                                     float *st_out, int32_t cfg);
+
+/* The tile config the calling thread's last GEMM launch dispatched (after the
+ * fallbacks above), so a test can assert which kernel it exercised. */
+BERT_API int32_t bertx_test_gemm_ran(void);
 
 /*
  * The f32 chain's GEMM (ftype 0 files: f32 activations x f32 weights on

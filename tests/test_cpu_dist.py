@@ -86,3 +86,23 @@ def test_algorithmic_bytes_bge_base_q4_0():
     w = 12 * (4 * 768 * 768 + 2 * 768 * 3072) * 0.5625
     rows = 64 * 512 * 768 * 0.5625
     assert w + rows < b < (w + rows) * 1.05
+
+
+def test_pmc_passes_skip_under_a_profiler(monkeypatch):
+    """bench.py never starts rocprofv3 from under a profiler: with a
+    rocprofv3 preload or its ROCPROF* variables in the environment, pmc_live reports
+    'skipped' and starts no process."""
+    import subprocess
+    import bench
+    assert not bench.under_profiler({"LD_PRELOAD": "", "PATH": "/usr/bin"})
+    assert bench.under_profiler({"LD_PRELOAD": "/opt/rocm/lib/rocprofiler-sdk/librocprofiler-sdk-tool.so"})
+    assert bench.under_profiler({"ROCPROF_KERNEL_TRACE": "1"})
+    assert bench.under_profiler({"ROCPROFILER_LIBRARY_CTOR": "1"})
+    monkeypatch.setenv("ROCPROF_OUTPUT_PATH", "/tmp/x")
+
+    def refuse(*a, **k):
+        raise AssertionError("a process was started under the profiler")
+
+    monkeypatch.setattr(subprocess, "run", refuse)
+    r = bench.pmc_live("/nonexistent.bin", 1, 32)
+    assert "skipped" in r and "bytes_per_forward" not in r

@@ -89,3 +89,43 @@ def test_matches_oracle_and_batch_stage(bert_vocab_model, host_ctx):
         assert lib.bertx_tokenize_batch(host_ctx.ctx, thr, len(tx), arr, 512, ids.ctypes.data, lens.ctypes.data) == 0
         for i, (ref, n) in enumerate(single):
             assert lens[i] == n and list(ids[i, :min(n, 512)]) == ref, (thr, i)
+
+
+def test_batch_stage_in_a_forked_child(host_ctx):
+    """The tokenizer pool (csrc/task_pool.cpp) after fork: the child has none of the
+    parent's pool threads; pthread_atfork gives it a fresh pool, so a multi-threaded
+    batch in the child finishes with the parent's ids instead of waiting forever on
+    workers that do not exist."""
+    lib = host_ctx.lib
+    tx = texts()[:64]
+    arr = (ctypes.c_char_p * len(tx))(*tx)
+    want = np.zeros((len(tx), 512), np.int32)
+    wl = np.zeros(len(tx), np.int32)
+    assert lib.bertx_tokenize_batch(host_ctx.ctx, 8, len(tx), arr, 512, want.ctypes.data, wl.ctypes.data) == 0
+    pid = os.fork()
+    if pid == 0:                                   # child: exit code 0 only on equal ids
+        rc = 1
+        try:
+            ids = np.zeros_like(want)
+            lens = np.zeros_like(wl)
+            ok = lib.bertx_tokenize_batch(host_ctx.ctx, 8, len(tx), arr, 512, ids.ctypes.data, lens.ctypes.data) == 0
+            rc = 0 if ok and np.array_equal(ids, want) and np.array_equal(lens, wl) else 1
+        finally:
+            os._exit(rc)
+    deadline = 60.0
+    import time
+    t0 = time.time()
+    while True:
+        done, status = os.waitpid(pid, os.WNOHANG)
+        if done:
+            break
+        if time.time() - t0 > deadline:
+            os.kill(pid, 9)
+            os.waitpid(pid, 0)
+            pytest.fail("the forked child's tokenizer batch hung")
+        time.sleep(0.05)
+    assert os.WIFEXITED(status) and os.WEXITSTATUS(status) == 0
+    # and the parent's pool still works
+    ids = np.zeros_like(want)
+    assert lib.bertx_tokenize_batch(host_ctx.ctx, 8, len(tx), arr, 512, ids.ctypes.data, wl.ctypes.data) == 0
+    assert np.array_equal(ids, want)

@@ -338,3 +338,61 @@ def test_c5_ragged_over_8_replicas(tmp_path, monkeypatch):
     assert sum(toks) == sum(lens) and len(set(toks)) > 1, per   # ragged shards
     assert max(p[0] for p in per) > 0.0
     assert np.array_equal(eight, one)
+
+
+def test_routing_small_calls_to_distinct_replicas(quant_models, monkeypatch):
+    """Serving on several replicas (bert_abi.cpp run_forward routing): a
+    call below 8,192 tokens per replica goes whole to the least-loaded replica (ties
+    rotate), so 4 sequential small calls use the 4 replicas once each, and 4 concurrent
+    callers (ctypes releases the GIL) land on distinct replicas -- every reply bitwise
+    equal to the single-replica result; a call of >= 4 x 8,192 tokens still spreads
+    over all 4 (bertx_device_calls counts the calls each replica ran)."""
+    import threading
+    path = quant_models[("tiny64", "q4_0")]
+    batches = [ragged_ids(690, [5, 40, 129, 300], seed=s) for s in range(8)]
+    monkeypatch.setenv("BERT_DEVICES", "0")
+    one = bertpy.BertModel(path)
+    want = [one.forward_batch(b) for b in batches]
+    del one
+    monkeypatch.setenv("BERT_DEVICES", "0,0,0,0")
+    m4 = bertpy.BertModel(path)
+    assert m4.lib.bertx_num_devices(m4.ctx) == 4
+
+    def calls():
+        return [m4.lib.bertx_device_calls(m4.ctx, i) for i in range(4)]
+
+    c0 = calls()
+    for b, w in zip(batches[:4], want[:4]):
+        assert np.array_equal(m4.forward_batch(b), w)
+    c1 = calls()
+    assert [b - a for a, b in zip(c0, c1)] == [1, 1, 1, 1], (c0, c1)
+    # concurrent: each of 4 threads sends its own small batches
+    got = [None] * 8
+    errors = []
+
+    def client(k):
+        try:
+            for j in (k, k + 4):
+                got[j] = m4.forward_batch(batches[j])
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=client, args=(k,)) for k in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert not errors, errors
+    for g, w in zip(got, want):
+        assert np.array_equal(g, w)
+    c2 = calls()
+    assert sum(c2) - sum(c1) == 8 and all(b > a for a, b in zip(c1, c2)), (c1, c2)
+    # a large call spreads: 64 sentences x 512 tokens = 32,768 tokens = 4 shares
+    big = ragged_ids(690, [512] * 64, seed=21)
+    monkeypatch.setenv("BERT_DEVICES", "0")
+    ref = bertpy.BertModel(path).forward_batch(big)
+    out = m4.forward_batch(big)
+    c3 = calls()
+    assert [b - a for a, b in zip(c2, c3)] == [1, 1, 1, 1], (c2, c3)
+    assert [p[1] for p in m4.device_last_call()] == [16] * 4
+    assert np.array_equal(out, ref)

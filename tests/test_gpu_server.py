@@ -33,13 +33,16 @@ def _recv_exact(sock, n):
     return buf
 
 
-def test_microbatch_server_concurrent_clients(quant_models):
+@pytest.mark.parametrize("devices", ["0", "0,0,0,0"])
+def test_microbatch_server_concurrent_clients(quant_models, devices):
+    """One replica (one batcher), and four replicas on the one GPU (BERT_DEVICES=0,0,0,0:
+    four batchers, each micro-batch routed whole to the least-loaded replica)."""
     if not os.path.exists(EXE):
         pytest.skip(f"{EXE} not built")
     path = quant_models[("tiny64", "q4_0")]
     env = dict(os.environ)
     env.pop("BERT_HOST_ONLY", None)
-    env["BERT_DEVICES"] = "0"
+    env["BERT_DEVICES"] = devices
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
@@ -82,6 +85,7 @@ def test_microbatch_server_concurrent_clients(quant_models):
         proc.kill()
         proc.wait(timeout=30)
 
+    os.environ["BERT_DEVICES"] = "0"
     m = bertpy.BertModel(path)
     o = oracle_lib.Oracle(path)
     for k in range(n_cli):
