@@ -93,12 +93,14 @@ namespace {
 
 constexpr int64_t kChunkTokens = 1 << 17;   // tokens per device forward (workspace bound)
 constexpr int kChunkSeqs = 4096;            // sentences per device forward (pool / output staging bound)
-// A call is split over k replicas only when each share keeps at least this many
-// tokens: below it a forward is launch- and latency-bound (C2's 4,096 tokens run in
-// 0.37 ms, B = 1 in 0.56 ms), so splitting a small batch buys little latency and
-// costs every replica a forward; it goes whole to the least-loaded replica instead,
-// and concurrent callers (the server's batchers) land on different replicas.
-constexpr int64_t kMinShareTokens = 8192;
+// A call is split only over replicas that are idle (no routed work in flight), and
+// only while each share keeps at least kMinShareTokens: below that a forward is
+// launch- and latency-bound (C2's 4,096 tokens run in 0.37 ms, B = 1 in 0.56 ms),
+// so a smaller share buys little latency and costs its replica a whole forward.  A
+// call that finds no idle replica goes whole to the least-loaded one, so concurrent
+// callers (the server's batchers) land on different replicas instead of all
+// splitting over all of them in lockstep.
+constexpr int64_t kMinShareTokens = 4096;
 
 std::vector<int> parse_device_list(int n_visible)
 {
@@ -132,9 +134,9 @@ double sentence_cost(const emb::HParams &hp, int L)
 }
 
 // Runs n sentences on the context's GPUs.  Routing (kMinShareTokens): the call
-// uses k = min(replicas, tokens / kMinShareTokens) (at least 1) replicas, the k
-// least-loaded by the cost still in flight on them (ties rotate, so consecutive
-// small calls spread over the replicas too); its sentences are split over those k
+// uses k = min(idle replicas, sentences, tokens / kMinShareTokens) (at least 1)
+// replicas, the k least-loaded by the cost still in flight on them (ties rotate,
+// so consecutive small calls spread over the replicas too); its sentences are split over those k
 // by cost, longest first to the least-loaded share (LPT).  Each replica walks its
 // sentences in chunks of <= kChunkTokens on its persistent worker thread (the
 // caller runs one share itself).  Results are independent of the routing and the
@@ -152,12 +154,14 @@ int run_forward(bert_ctx *ctx, const int32_t *const *toks, const int32_t *lens, 
     std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return lens[a] > lens[b]; });
     int64_t tokens = 0;
     for (int i = 0; i < n; ++i) tokens += lens[i];
-    const int k = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)nd, (int64_t)n, tokens / kMinShareTokens}));
     std::vector<std::vector<int>> assign((size_t)nd);
     std::vector<double> load((size_t)nd, 0.0);
     std::vector<int> chosen((size_t)nd);
     {
         std::lock_guard<std::mutex> lk(ctx->route_mu);
+        int64_t idle = 0;
+        for (double w : ctx->inflight) idle += w == 0.0 ? 1 : 0;
+        const int k = (int)std::max<int64_t>(1, std::min<int64_t>({idle, (int64_t)n, tokens / kMinShareTokens}));
         std::iota(chosen.begin(), chosen.end(), 0);
         const unsigned rot = ctx->rr;
         std::stable_sort(chosen.begin(), chosen.end(), [&](int a, int b) {
@@ -210,7 +214,7 @@ int run_forward(bert_ctx *ctx, const int32_t *const *toks, const int32_t *lens, 
     auto finish = [&](int dv) {
         std::lock_guard<std::mutex> lk(ctx->route_mu);
         ctx->inflight[(size_t)dv] -= load[(size_t)dv];
-        if (ctx->inflight[(size_t)dv] < 0.5) ctx->inflight[(size_t)dv] = 0.0;   // no drift from float sums
+        if (ctx->inflight[(size_t)dv] < 0.5) ctx->inflight[(size_t)dv] = 0.0;   // idle again (no float drift)
     };
     std::vector<int> used;
     for (int dv : chosen) if (!assign[(size_t)dv].empty()) used.push_back(dv);

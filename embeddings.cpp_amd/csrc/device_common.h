@@ -41,6 +41,12 @@ __device__ __forceinline__ float halves_sum(float x)
     return a + b;
 }
 
+// LDS byte address of a pointer into __shared__ memory
+__device__ __forceinline__ uint32_t lds_u32(const void *p)
+{
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char *)p;
+}
+
 __device__ __forceinline__ h16x2 as_h2(uint32_t u) { return __builtin_bit_cast(h16x2, u); }
 __device__ __forceinline__ h16 as_h(uint16_t u) { return __builtin_bit_cast(h16, u); }
 // (x & vmask) | smagic as ONE v_and_or_b32: gfx9 VOP3 encodes no literal and reads at

@@ -50,11 +50,6 @@ __device__ unsigned long long g_gemm_stamps[1 << 18];
 
 namespace {
 
-__device__ __forceinline__ uint32_t lds_u32(const void *p)
-{
-    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char *)p;
-}
-
 // ds_read_b128 at base + OFF with the read's completion tracked by hand: the
 // asm keeps the issue order (hipcc's scheduler otherwise moves every read down
 // next to its MFMAs), zwait_lgkm ties the data to a counted s_waitcnt.
@@ -677,8 +672,18 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
                             pw[e] = __builtin_bit_cast(uint32_t, h16x2{(h16)v[a][2 * e], (h16)v[a][2 * e + 1]});
                     }
                     h16 *const dst = (h16 *)out + (size_t)tok * N + cb + 16 * a;
-                    if (ln.store_nt) {
-                        typedef uint32_t u32x4n __attribute__((ext_vector_type(4)));
+                    typedef uint32_t u32x4n __attribute__((ext_vector_type(4)));
+                    if (ln.store_nt >= 2) {
+                        // write-through stores that drop the line from the XCD's L2
+                        // (cache policy sc1, 2: or sc0 sc1, 3; MI355X_MICROARCH.md
+                        // store flavours): the output does not evict the X panels and
+                        // weights the XCD's next tiles read
+                        const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+                            (void *)((h16 *)out + (size_t)m0 * N), (short)0, BM * N * 2, 0x00020000);
+                        const int vo = ((tok - m0) * N + cb + 16 * a) * 2;
+                        if (ln.store_nt == 2) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4n, pk), ors, vo, 0, 16);
+                        else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4n, pk), ors, vo, 0, 17);
+                    } else if (ln.store_nt) {
                         __builtin_nontemporal_store(__builtin_bit_cast(u32x4n, pk), (u32x4n *)dst);
                     } else {
                         *(uint4 *)dst = pk;
@@ -689,8 +694,8 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     }
 }
 
-template <int FMT, int EPI, bool LNF, int NW, int BM, int NS, int FA, int WR, int NT, int XI>
-__global__ __launch_bounds__(64 * NW, 2) void gemmz_kernel(DevWeight W, const h16 *__restrict__ X,
+template <int FMT, int EPI, bool LNF, int NW, int BM, int NS, int FA, int WR, int NT, int XI, int OCC>
+__global__ __launch_bounds__(64 * NW, OCC * NW / 4) void gemmz_kernel(DevWeight W, const h16 *__restrict__ X,
                                                                const float *__restrict__ bias,
                                                                const void *__restrict__ res, void *__restrict__ out,
                                                                int nN, int nTiles, LnFold ln)
@@ -708,7 +713,9 @@ __global__ __launch_bounds__(64 * NW, 2) void gemmz_kernel(DevWeight W, const h1
     }
 }
 
-template <int FMT, int NW, int BM, int NS, int FA = 1, int WR = 3, int NT = 1, int XI = 0>
+// OCC: workgroups per CU the launch bounds ask registers for (2: two co-resident
+// tiles; 3: three, at most 168 VGPRs per wave)
+template <int FMT, int NW, int BM, int NS, int FA = 1, int WR = 3, int NT = 1, int XI = 0, int OCC = 2>
 void dispatch_z(const DevWeight &W, const h16 *x, int M, const float *bias, int epi, const void *res, void *out,
                 hipStream_t s, const LnFold &ln, bool lnf)
 {
@@ -722,19 +729,19 @@ void dispatch_z(const DevWeight &W, const h16 *x, int M, const float *bias, int 
     // column tiles only.  BERT_GEMM_PERSIST = k forces k per CU, 0 = off.
     static const int persist_env = [] { const char *e = std::getenv("BERT_GEMM_PERSIST"); return e ? std::atoi(e) : -1; }();
     const int cus = device_cu_count();
-    const int persist = persist_env >= 0 ? persist_env : (nTiles <= 4 * cus ? 2 : 0);
+    const int persist = persist_env >= 0 ? persist_env : (nTiles <= 2 * OCC * cus ? OCC : 0);
     int grid = nTiles;
     if (persist > 0 && W.N % BN == 0) grid = std::min(nTiles, persist * cus);
     auto go = [&](auto kern) { kern<<<grid, 64 * NW, 0, s>>>(W, x, bias, res, out, nN, nTiles, ln); };
     if (epi == EPI_BIAS_F16) {
-        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_F16, true, NW, BM, NS, FA, WR, NT, XI>);
-        else go(gemmz_kernel<FMT, EPI_BIAS_F16, false, NW, BM, NS, FA, WR, NT, XI>);
+        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_F16, true, NW, BM, NS, FA, WR, NT, XI, OCC>);
+        else go(gemmz_kernel<FMT, EPI_BIAS_F16, false, NW, BM, NS, FA, WR, NT, XI, OCC>);
     } else if (epi == EPI_BIAS_GELU_F16) {
-        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_GELU_F16, true, NW, BM, NS, FA, WR, NT, XI>);
-        else go(gemmz_kernel<FMT, EPI_BIAS_GELU_F16, false, NW, BM, NS, FA, WR, NT, XI>);
+        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_GELU_F16, true, NW, BM, NS, FA, WR, NT, XI, OCC>);
+        else go(gemmz_kernel<FMT, EPI_BIAS_GELU_F16, false, NW, BM, NS, FA, WR, NT, XI, OCC>);
     } else {
-        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_RES, true, NW, BM, NS, FA, WR, NT, XI>);
-        else go(gemmz_kernel<FMT, EPI_BIAS_RES, false, NW, BM, NS, FA, WR, NT, XI>);
+        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_RES, true, NW, BM, NS, FA, WR, NT, XI, OCC>);
+        else go(gemmz_kernel<FMT, EPI_BIAS_RES, false, NW, BM, NS, FA, WR, NT, XI, OCC>);
     }
 }
 
@@ -775,7 +782,8 @@ int launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, i
     // profiles/r03_attention_flow_ab.log nt rows; noise on another, r03_gemm_w8_nt_ab.log);
     // the small forms keep L2
     // stores (their next kernel reads the output while it is still there).
-    // BERT_GEMM_NT = 0 / 1 forces it off / on everywhere.
+    // BERT_GEMM_NT = 0 / 1 forces it off / on everywhere; 2 / 3: write-through
+    // stores with cache policy sc1 / sc0 sc1 (A/B).
     if (ln.store_nt < 0) ln.store_nt = (cfg == 2 || cfg == 11) ? 1 : 0;
     // 256 x 128: the X pieces among the MFMAs (one per B-fragment item from the
     // K-step's start; +1.2-1.6 % on the C3 forward over one burst in front of them,

@@ -68,9 +68,10 @@ BERT_API int32_t bertx_device_last_call(struct bert_ctx *ctx, int32_t slot, doub
  * Number of host-driven calls (bert_forward_batch / bert_encode_batch shares) that
  * have run on replica `slot` since load, or -1 for a bad slot.  Routing rule of
  * those calls (bert_abi.cpp run_forward): a call of T tokens uses
- * k = clamp(T / 8192, 1, replicas) replicas, the k least-loaded by the work still in
- * flight on them (ties rotate), split by cost; so concurrent small calls land on
- * different replicas and a large batch spreads over all of them.
+ * k = clamp(min(idle replicas, T / 4096), 1, ...) replicas, the k least-loaded by the
+ * work still in flight on them (ties rotate), split by cost; so a large batch
+ * spreads over the idle replicas and a call that finds none idle (a concurrent
+ * caller) goes whole to the least-loaded replica.
  */
 BERT_API int64_t bertx_device_calls(struct bert_ctx *ctx, int32_t slot);
 

@@ -342,10 +342,10 @@ def test_c5_ragged_over_8_replicas(tmp_path, monkeypatch):
 
 def test_routing_small_calls_to_distinct_replicas(quant_models, monkeypatch):
     """Serving on several replicas (bert_abi.cpp run_forward routing): a
-    call below 8,192 tokens per replica goes whole to the least-loaded replica (ties
-    rotate), so 4 sequential small calls use the 4 replicas once each, and 4 concurrent
-    callers (ctypes releases the GIL) land on distinct replicas -- every reply bitwise
-    equal to the single-replica result; a call of >= 4 x 8,192 tokens still spreads
+    call below 2 x 4,096 tokens goes whole to the least-loaded replica (ties rotate),
+    so 4 sequential small calls use the 4 replicas once each, and 4 concurrent callers
+    (ctypes releases the GIL) land on distinct replicas -- every reply bitwise equal to
+    the single-replica result; a call of >= 4 x 4,096 tokens on idle replicas spreads
     over all 4 (bertx_device_calls counts the calls each replica ran)."""
     import threading
     path = quant_models[("tiny64", "q4_0")]
