@@ -719,421 +719,6 @@ __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restr
 }
 
 
-// ---------------------------------------------------------------------------
-// attention_q64 (dh 64, L <= 512): the lds3 data path (whole K/V of a (sentence,
-// head) in LDS, persistent workgroup per CU walking the items, region A / B DMA
-// hidden under the previous half item) on 8 waves of 64 queries each -- two
-// 32-query groups g0 / g1 per wave, so every K and V fragment read from LDS
-// feeds two MFMAs and each wave has two independent chains to overlap.
-//
-// Why (profiles/r03_final_pmc_summary.txt): lds3 at 16 waves
-// x 128 VGPRs had no registers for read-ahead, so each QK MFMA waited on its own
-// ds_read (lgkmcnt(0) in front of every MFMA), and its waves ran in lockstep
-// phases (all four waves of a SIMD in QK, then all in the softmax): the matrix
-// pipe sat idle in the VALU phase and the VALU in the latency-bound QK phase.
-// Here a unit = 32 keys; per unit and wave: A(u) = QK^T of both groups (2 x (1
-// offset MFMA + 4)), B(u) = the softmax (exp2, row sums, f16 pack: ~80 VALU),
-// C(u) = P V (8 MFMAs).  The loop issues A(u + 1)'s MFMAs interleaved with
-// B(u)'s VALU in one basic block (sched_group_barrier), then C(u); the K
-// fragments of A(u + 2) are read ahead under C(u).
-// Numerics as lds3: Q pre-scaled by log2(e)/sqrt(dh), S - c from the MFMA (c =
-// the f16-rounded max of the first unit per query), P = exp2 rounded to f16 for
-// the MFMA, f32 row sums; a unit whose half-row sum passes 2^ATT_SUMX moves c to
-// its row max and rescales O, l and the already computed S(u + 1).
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(512) void attention_q64_kernel(const h16 *__restrict__ qkv, const int32_t *__restrict__ cu,
-                                                            int d, int nh, int n_items, float sl2,
-                                                            h16 *__restrict__ out)
-{
-    constexpr int DH = 64, RB = DH * 2, LMAX = ATT_LDS_MAX, RH = LMAX / 2, NU = LMAX / 32;
-    static_assert(RH == 256 && NU == 16, "two regions of 8 units");
-    __shared__ __attribute__((aligned(16))) char smem[2 * LMAX * RB];
-    char *const Kl = smem;
-    const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int hi = lane >> 5, lq = lane & 31;
-    const int ld = 3 * d;
-
-    struct Item { int start, len, h; };
-    auto item = [&](int i) {
-        const int b = i / nh;
-        Item r;
-        r.h = i - b * nh;
-        r.start = cu[b];
-        r.len = cu[b + 1] - r.start;
-        return r;
-    };
-    // region r (rows 256 r .. +255): piece i = rows 8 i .. 8 i + 7 of K and of V;
-    // wave w issues pieces 32 r + w + 8 j (j < 4) that hold rows of the sentence's
-    // 64-row blocks (swizzles as lds3)
-    auto issue = [&](const Item &it, int r) {
-        const int lane = lane_id_opaque();
-        const int nrows = (it.len + 63) & ~63;
-        const h16 *kbase = qkv + (size_t)it.start * ld + d + it.h * DH;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int i = 32 * r + w + 8 * j;
-            if (8 * i < nrows) {
-                const int row = 8 * i + (lane >> 3), pc = lane & 7;
-                const size_t so = (size_t)min(row, it.len - 1) * ld;
-                glds16_hidden(kbase + so + (pc ^ ((row >> 1) & 7)) * 8, Kl + i * 1024);
-                glds16_hidden(kbase + d + so + (pc ^ (((row >> 1) & 1) << 2)) * 8, Kl + LMAX * RB + i * 1024);
-            }
-        }
-    };
-    h16x8 qf[2][DH / 16];
-    auto load_q = [&](const Item &it) {                   // raw rows; scaled at the item's start
-        if (it.len <= 0) return;
-        const int lane = lane_id_opaque(), hi = lane >> 5, lq = lane & 31;
-#pragma unroll
-        for (int g = 0; g < 2; ++g) {
-            const h16 *qrow = qkv + (size_t)(it.start + min(64 * w + 32 * g + lq, it.len - 1)) * ld + it.h * DH;
-#pragma unroll
-            for (int st = 0; st < DH / 16; ++st) qf[g][st] = *(const h16x8 *)(qrow + 16 * st + 8 * hi);
-        }
-    };
-
-    // lane-constant LDS offsets (units are 32-row aligned)
-    int koff[DH / 16];
-#pragma unroll
-    for (int st = 0; st < DH / 16; ++st) koff[st] = lq * RB + (((2 * st + hi) ^ ((lq >> 1) & 7)) << 4);
-    const int gi = lane & 15, gq = gi >> 2, gp = gi & 3, gg = lane >> 4;
-    const int vsw = ((gq >> 1) & 1) << 2;
-    int voff[DH / 32];
-#pragma unroll
-    for (int t = 0; t < DH / 32; ++t) {
-        const int ch = 4 * t + 2 * (gg & 1) + (gp >> 1);
-        voff[t] = (4 * (gg >> 1) + gq) * RB + ((ch ^ vsw) << 4) + 8 * (gp & 1) + LMAX * RB;
-    }
-    const h16 one = (h16)1.0f, zero = (h16)0.0f;
-    const h16x8 abias = {hi ? zero : one, zero, zero, zero, zero, zero, zero, zero};
-    h16x8 bbias[2];
-
-    f32x16 o[2][DH / 32];
-    float c[2], l[2];
-    f32x16 sa[2], sb[2];                                  // S of two consecutive units (ping-pong)
-    h16x8 kf[DH / 16];                                    // K fragments of the next unit
-    int len = 0;
-
-    auto mask = [&](f32x16 (&S)[2], int u) {              // keys past the sentence -> -inf (P exactly 0)
-        if (32 * u + 32 > len) {
-#pragma unroll
-            for (int g = 0; g < 2; ++g)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int key = 32 * u + (r & 3) + 8 * (r >> 2) + 4 * hi;
-                    if (key >= len) S[g][r] = -INFINITY;
-                }
-        }
-    };
-    // B: P = f16(exp2(S)), this half's row sums (two chains per group)
-    h16x8 pp[2][2];
-    auto softmax = [&](f32x16 (&S)[2], float (&rs)[2]) {
-#pragma unroll
-        for (int g = 0; g < 2; ++g) {
-            float r0 = 0.f, r1 = 0.f;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float p = __builtin_amdgcn_exp2f(S[g][r]);
-                S[g][r] = p;
-                if (r & 1) r1 += p;
-                else r0 += p;
-            }
-            rs[g] = r0 + r1;
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-                for (int j = 0; j < 8; ++j) pp[g][s2][j] = (h16)S[g][8 * s2 + j];
-        }
-    };
-    // C: O += V^T P^T of both groups (each V fragment feeds the two).  All eight
-    // transposing reads of the unit are issued first (asm: order kept), each
-    // operand waited for right before its MFMA pair (counted lgkmcnt), so their
-    // latencies overlap instead of one per MFMA pair.
-    uint32_t vad[DH / 32];
-#pragma unroll
-    for (int t = 0; t < DH / 32; ++t) vad[t] = lds_u32(smem) + (uint32_t)voff[t];
-    auto pv = [&](int u) {
-        typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
-        u32x2v lo[4], up[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {                     // operand i = (s2 = i / 2, t = i % 2)
-            const uint32_t a = vad[i & 1] + (uint32_t)((32 * u + 16 * (i >> 1)) * RB);
-            asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo[i]) : "v"(a));
-            asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(up[i]) : "v"(a), "i"(8 * RB));
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            switch (i) {
-            case 0: asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(lo[0]), "+v"(up[0])); break;
-            case 1: asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(lo[1]), "+v"(up[1])); break;
-            case 2: asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(lo[2]), "+v"(up[2])); break;
-            default: asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lo[3]), "+v"(up[3])); break;
-            }
-            const h16x4 l4 = __builtin_bit_cast(h16x4, lo[i]), u4 = __builtin_bit_cast(h16x4, up[i]);
-            const h16x8 va = {l4[0], l4[1], l4[2], l4[3], u4[0], u4[1], u4[2], u4[3]};
-#pragma unroll
-            for (int g = 0; g < 2; ++g)
-                o[g][i & 1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(va, pp[g][i >> 1], o[g][i & 1], 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);            // the next wait stays behind this pair
-        }
-    };
-    // K-fragment base addresses (LDS byte addresses, lane constants)
-    uint32_t kad[DH / 16];
-#pragma unroll
-    for (int st = 0; st < DH / 16; ++st) kad[st] = lds_u32(Kl) + (uint32_t)koff[st];
-    // B(u) on S with A(u + 1) into Sn, interleaved (see the unit loop)
-    auto interleaved = [&](int u, f32x16 (&S)[2], f32x16 (&Sn)[2], float (&rs)[2]) {
-        const uint32_t ko = (uint32_t)(32 * (u + 1) * RB);
-#pragma unroll
-        for (int st = 0; st < DH / 16; ++st)
-            asm volatile("ds_read_b128 %0, %1" : "=v"(kf[st]) : "v"(kad[st] + ko));
-#pragma unroll
-        for (int g = 0; g < 2; ++g) Sn[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(abias, bbias[g], f32x16{}, 0, 0, 0);
-        float r0[2] = {0.f, 0.f}, r1[2] = {0.f, 0.f};
-        __builtin_amdgcn_sched_barrier(0);
-        // windows: exponentials of a quarter of B(u), then the MFMA pair of the K
-        // fragment read longest ago (the reads' latency under the first window)
-#pragma unroll
-        for (int st = 0; st <= DH / 16; ++st) {
-            if (st < DH / 16) {
-#pragma unroll
-                for (int g = 0; g < 2; ++g)
-#pragma unroll
-                    for (int r = 4 * st; r < 4 * st + 4; ++r) {
-                        const float p = __builtin_amdgcn_exp2f(S[g][r]);
-                        S[g][r] = p;
-                        if (r & 1) r1[g] += p;
-                        else r0[g] += p;
-                    }
-            }
-            if (st > 0) {
-                const int k = st - 1;
-                switch (k) {                              // K fragment k has landed
-                case 0: asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(kf[0])); break;
-                case 1: asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(kf[1])); break;
-                case 2: asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(kf[2])); break;
-                default: asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(kf[3])); break;
-                }
-#pragma unroll
-                for (int g = 0; g < 2; ++g) Sn[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[k], qf[g][k], Sn[g], 0, 0, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-#pragma unroll
-        for (int g = 0; g < 2; ++g) {
-            rs[g] = r0[g] + r1[g];
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-                for (int j = 0; j < 8; ++j) pp[g][s2][j] = (h16)S[g][8 * s2 + j];
-        }
-        // B(u) complete here: nothing of it sinks past the branches that follow
-        asm volatile("" ::"v"(pp[0][0]), "v"(pp[0][1]), "v"(pp[1][0]), "v"(pp[1][1]), "v"(rs[0]), "v"(rs[1]));
-    };
-    // A(u) alone (unit 0, the rare offset move): the four K fragments read first,
-    // each waited for right before its MFMA pair
-    auto qk_counted = [&](int u, f32x16 (&S)[2], bool bias) {
-        const uint32_t ko = (uint32_t)(32 * u * RB);
-#pragma unroll
-        for (int st = 0; st < DH / 16; ++st)
-            asm volatile("ds_read_b128 %0, %1" : "=v"(kf[st]) : "v"(kad[st] + ko));
-#pragma unroll
-        for (int g = 0; g < 2; ++g)
-            S[g] = bias ? __builtin_amdgcn_mfma_f32_32x32x16_f16(abias, bbias[g], f32x16{}, 0, 0, 0) : f32x16{};
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int st = 0; st < DH / 16; ++st) {
-            switch (st) {
-            case 0: asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(kf[0])); break;
-            case 1: asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(kf[1])); break;
-            case 2: asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(kf[2])); break;
-            default: asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(kf[3])); break;
-            }
-#pragma unroll
-            for (int g = 0; g < 2; ++g) S[g] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[st], qf[g][st], S[g], 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    };
-    auto row_max = [&](const f32x16 &S) {
-        float mx = S[0];
-#pragma unroll
-        for (int r = 1; r < 16; ++r) mx = fmaxf(mx, S[r]);
-        return halves_max(mx);
-    };
-    // after B(u): a half-row sum past 2^ATT_SUMX (rare) moves the offset to the row
-    // max and redoes unit u; S(u + 1) (computed with the old offset) is shifted too
-    auto check = [&](f32x16 (&S)[2], f32x16 (&Sn)[2], float (&rs)[2], int u, bool has_next) {
-        const float lim = (float)(1 << ATT_SUMX);
-        if (__builtin_amdgcn_ballot_w64(rs[0] > lim || rs[1] > lim)) {
-            qk_counted(u, S, true);
-            mask(S, u);
-#pragma unroll
-            for (int g = 0; g < 2; ++g) {
-                const float m = row_max(S[g]);
-                const float sh = m > 0.f ? (float)(h16)(c[g] + m) - c[g] : 0.f;
-                const float alpha = __builtin_amdgcn_exp2f(-sh);
-#pragma unroll
-                for (int r = 0; r < 16; ++r) S[g][r] -= sh;
-                if (has_next)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) Sn[g][r] -= sh;
-                c[g] += sh;
-                bbias[g][0] = hi ? zero : (h16)(-c[g]);
-                l[g] *= alpha;
-#pragma unroll
-                for (int t = 0; t < DH / 32; ++t)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) o[g][t][r] *= alpha;
-            }
-            softmax(S, rs);
-        }
-        l[0] += rs[0];
-        l[1] += rs[1];
-    };
-
-    int cur_i = blockIdx.x;
-    if (cur_i >= n_items) return;                         // workgroup-uniform
-    Item cur = item(cur_i);
-    load_q(cur);
-    issue(cur, 0);
-    wait_all_vm();
-    __syncthreads();
-    const h16 s16 = (h16)sl2;
-    const h16x8 sc = {s16, s16, s16, s16, s16, s16, s16, s16};
-#ifdef ATT_STAMPS
-    int nit = 0;
-#endif
-    for (;;) {
-        ASTAMP(0, __builtin_amdgcn_s_memtime());
-        const int nx_i = cur_i + (int)gridDim.x;
-        const bool more = nx_i < n_items;                 // workgroup-uniform
-        Item nx = {0, 0, 0};
-        if (more) nx = item(nx_i);
-        len = cur.len;
-        const int nu = ((len + 63) & ~63) / 32;           // units with loaded rows
-        const bool active = 64 * w < len;                 // wave-uniform
-#pragma unroll
-        for (int g = 0; g < 2; ++g)
-#pragma unroll
-            for (int st = 0; st < DH / 16; ++st) qf[g][st] *= sc;
-        asm volatile("" ::"v"(qf[0][0]), "v"(qf[1][0]), "v"(qf[0][3]), "v"(qf[1][3]));
-        issue(cur, 1);                                    // region B (behind Q's wait)
-#pragma unroll
-        for (int g = 0; g < 2; ++g) {
-#pragma unroll
-            for (int t = 0; t < DH / 32; ++t)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) o[g][t][r] = 0.f;
-            c[g] = 0.f;
-            l[g] = 0.f;
-            bbias[g] = h16x8{zero, zero, zero, zero, zero, zero, zero, zero};
-        }
-        if (active) {
-            // unit 0: its row max is the offset (f16-rounded); then B(0) with A(1)
-            // interleaved, as every later unit
-            float rs[2];
-            qk_counted(0, sa, false);
-            mask(sa, 0);
-#pragma unroll
-            for (int g = 0; g < 2; ++g) {
-                c[g] = (float)(h16)row_max(sa[g]);
-#pragma unroll
-                for (int r = 0; r < 16; ++r) sa[g][r] -= c[g];
-                bbias[g][0] = hi ? zero : (h16)(-c[g]);
-            }
-            interleaved(0, sa, sb, rs);
-            if (nu > 1) mask(sb, 1);
-            l[0] = rs[0];
-            l[1] = rs[1];
-            pv(0);
-        }
-        ASTAMP(1, __builtin_amdgcn_s_memtime());
-        // units 1 .. 15: B(u) with A(u + 1) interleaved, then C(u); S ping-pongs
-        // between sa (even units) and sb (odd units)
-        auto unit = [&](int u, f32x16 (&S)[2], f32x16 (&Sn)[2]) {
-            if (u == 7) {
-                ASTAMP(2, __builtin_amdgcn_s_memtime());
-                wait_all_vm();                            // this wave's region-B pieces
-                __syncthreads();                          // B1a: region B landed for every wave
-                ASTAMP(3, __builtin_amdgcn_s_memtime());
-            }
-            if (active && u < nu) {
-                // A(u + 1) unconditionally (one basic block with B(u)): past the
-                // sentence's loaded rows (or the image, u = 15) it reads finite LDS
-                // bytes of no consequence -- that S is never used.  The K fragments
-                // are asm reads issued first, each waited for right before its MFMA
-                // pair (counted lgkmcnt); between the pairs, a quarter of B(u)'s
-                // exponentials in fixed windows (sched_barrier), so the matrix pipe
-                // and the VALU work side by side within the wave.
-                float rs[2];
-                interleaved(u, S, Sn, rs);
-                if (u + 1 < nu) mask(Sn, u + 1);
-                check(S, Sn, rs, u, u + 1 < nu);
-                pv(u);
-            }
-            if (u == 8) {
-                ASTAMP(4, __builtin_amdgcn_s_memtime());
-                __syncthreads();                          // B1b: every wave is past region A
-                if (more) issue(nx, 0);
-            }
-        };
-#pragma clang loop unroll(disable)
-        for (int u = 1; u < NU; u += 2) {
-            unit(u, sb, sa);
-            if (u + 1 < NU) unit(u + 1, sa, sb);
-        }
-        ASTAMP(5, __builtin_amdgcn_s_memtime());
-        if (more) load_q(nx);
-        if (more) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // the 8 Q loads younger
-        else wait_all_vm();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __syncthreads();                                  // S: region B is free
-        ASTAMP(6, __builtin_amdgcn_s_memtime());
-        if (active) {
-            // lane (q, hi) holds dh 8m + 4 hi .. +3 of chunks m; one
-            // v_permlane32_swap per dword of a chunk pair gives each lane 16
-            // contiguous bytes (four 16-B stores per group), as lds3
-            const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
-                (void *)(out + (size_t)cur.start * d), (short)0, cur.len * d * 2, 0x00020000);
-#pragma unroll
-            for (int g = 0; g < 2; ++g) {
-                const float inv = 1.0f / halves_sum(l[g]);
-                const int q = 64 * w + 32 * g + lq;
-                uint32_t pk[DH / 8][2];
-#pragma unroll
-                for (int m = 0; m < DH / 8; ++m)
-#pragma unroll
-                    for (int k = 0; k < 2; ++k) {
-                        const int t = m >> 2, gq4 = m & 3;
-                        const h16x2 v = {(h16)(o[g][t][4 * gq4 + 2 * k] * inv), (h16)(o[g][t][4 * gq4 + 2 * k + 1] * inv)};
-                        pk[m][k] = __builtin_bit_cast(uint32_t, v);
-                    }
-#pragma unroll
-                for (int p = 0; p < DH / 16; ++p)
-#pragma unroll
-                    for (int k = 0; k < 2; ++k) {
-                        const auto r = __builtin_amdgcn_permlane32_swap(pk[2 * p][k], pk[2 * p + 1][k], false, false);
-                        pk[2 * p][k] = r[0];
-                        pk[2 * p + 1][k] = r[1];
-                    }
-                const int ob = (q * d + cur.h * DH + 8 * hi) * 2;
-#pragma unroll
-                for (int p = 0; p < DH / 16; ++p) {
-                    typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
-                    const u32x4v v = {pk[2 * p][0], pk[2 * p][1], pk[2 * p + 1][0], pk[2 * p + 1][1]};
-                    __builtin_amdgcn_raw_buffer_store_b128(v, ors, ob + 32 * p, 0, 0);
-                }
-            }
-        }
-        ASTAMP(7, __builtin_amdgcn_s_memtime());
-#ifdef ATT_STAMPS
-        ++nit;
-#endif
-        if (!more) break;
-        cur = nx;
-        cur_i = nx_i;
-    }
-}
 
 thread_local int g_att_variant = 0;   // benches only (bertx_bench_attention), per calling thread
 
@@ -1145,18 +730,11 @@ void launch_attention(const uint16_t *qkv, const int32_t *cu, int32_t n_seqs, in
     if (max_len <= ATT_LDS_MAX && (dh == 64 || dh == 32)) {
         const dim3 g(n_seqs * n_head), blk(1024);
         if (dh == 64) {
-            // 0: production, 7: the same kernel on at most 7 workgroups (tests: many
-            // ragged items each); 8 / 9: attention_q64 (8 waves x 64 queries) on
-            // every CU / on 7 workgroups; BERT_ATT_Q64=1 makes q64 the production
-            // kernel (A/B)
+            // 0: production (attention_lds3, persistent, one workgroup per CU); 7:
+            // the same kernel on at most 7 workgroups (tests: many ragged items each)
             const int n_items = n_seqs * n_head;
-            const int cap = (g_att_variant == 7 || g_att_variant == 9) ? 7 : device_cu_count();
+            const int cap = g_att_variant == 7 ? 7 : device_cu_count();
             const int grid = n_items < cap ? n_items : cap;
-            static const bool q64_env = [] { const char *e = std::getenv("BERT_ATT_Q64"); return e && *e == '1'; }();
-            if ((g_att_variant == 8 || g_att_variant == 9 || (q64_env && g_att_variant != 7)) && grid > 0) {
-                attention_q64_kernel<<<grid, 512, 0, s>>>((const h16 *)qkv, cu, d, n_head, n_items, sl2, (h16 *)out);
-                return;
-            }
             // stores after the S barrier (default); BERT_ATT_EARLY_STORE=1 stores
             // before it -- measured 2 us slower at C3 (70.3 vs 72.6 us,
             // profiles/r03_attention_store_ab.log): the early stores compete with

@@ -323,6 +323,11 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
         xvo[i] = (uint32_t)(r * KX + (((lane & 7) ^ ((r >> 1) & 7)) * 8)) * 2u;
     }
     auto issue_x_piece = [&](int ks, int stage, int i) {
+#if defined(GEMM_ABLATE) && (GEMM_ABLATE & 1)
+        // diagnostic build only: no X staging (wrong results; the K loop's cost
+        // without its LDS-DMA pieces)
+        if (ks > 0) return;
+#endif
         char *dst = PRIV ? smem + (wave * NS + stage) * XBW : smem + stage * XB + ((8 * XG * wave) << 7);
         const int kc = ks < KSX ? ks : ks - KSX;   // the X column block of K-step ks
         __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_void_t *)(dst + (i << 10)), 16, xvo[i & 1],
