@@ -71,12 +71,21 @@ struct ZRegsQ4 {
         const h16x2 d2 = {dh, dh};
         h16x2 m2 = {(h16)0.0f, (h16)0.0f};
         if (FMT == FMT_Q4_1) { const h16 mh = zh(m, u); m2 = h16x2{mh, mh}; }
-        const h16 o = FMT == FMT_Q4_1 ? (h16)-1024.0f : (h16)-1032.0f;
-        const h16x2 off = {o, o};
+        // Pair p's nibbles sit at bits 4p'.. of each half (p' = p mod 2 after a shift
+        // by 8 for p >= 2).  Bits 0-3 are the low mantissa bits of 0x6400 (1024,
+        // ulp 1): 1024 + q; bits 4-7 are mantissa bits 4-7 of 0x5400 (64, ulp 1/16):
+        // 64 + q.  So one shift per fragment instead of three; the offset add is exact
+        // either way and the value (q - 8) d (q d + m) is rounded once, as before.
+        const h16 o0 = FMT == FMT_Q4_1 ? (h16)-1024.0f : (h16)-1032.0f;
+        const h16 o1 = FMT == FMT_Q4_1 ? (h16)-64.0f : (h16)-72.0f;
+        const h16x2 off0 = {o0, o0}, off1 = {o1, o1};
+        const uint32_t w8 = w >> 8;
         h16x8 a;
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
-            h16x2 hh = as_h2(and_or_vs(w >> (4 * p), 0x000F000Fu, 0x64006400u)) + off;
+            const uint32_t x = p < 2 ? w : w8;
+            h16x2 hh = (p & 1) ? as_h2(and_or_vs(x, 0x00F000F0u, 0x54005400u)) + off1
+                               : as_h2(and_or_vs(x, 0x000F000Fu, 0x64006400u)) + off0;
             hh = FMT == FMT_Q4_1 ? hh * d2 + m2 : hh * d2;
             a[2 * p] = hh[0];
             a[2 * p + 1] = hh[1];
