@@ -1,7 +1,7 @@
 // Memory-bound row kernels: embeddings + LayerNorm, the LayerNorm statistics
 // of the residual stream, mean pool + L2 (the LN fold of kernels.h).
-// Embeddings: one 16-lane group per token row; each lane owns 4 consecutive
-// features per 64-wide slice (16-B loads and stores), reductions by shuffles.
+// Embeddings: one 32-lane group per token row, one 32-wide quant block per lane,
+// reductions by shuffles.
 #include "device_common.h"
 #include "host_common.h"
 #include "kernels.h"
@@ -15,92 +15,89 @@ namespace emb {
 namespace {
 
 
-// One row per 16-lane group (4 rows per wave, 16 per block): each lane owns 4
-// consecutive features of every 64-wide slice, so all of a row's table loads are
-// in flight at once and the two reductions are 4 xor-shuffles each (a wave per
-// row with 64-lane reductions: 57 us at C3, latency-bound).
-constexpr int EMB_MAXS = 16;   // slices of 64 features: n_embd <= 1024
+// One row per 32-lane group, one 32-wide quant block per lane (8 rows per 256-thread
+// block, n_embd <= 1024): each lane reads its block of the three tables with a few
+// wide loads (table_read.h) and keeps the 32 f32 values in registers, the two
+// reductions are xor-shuffles inside the group.  No LDS and no barrier, so a row
+// costs one dependent load chain (ids -> table rows) and the loads of every row in
+// flight at once (the LDS-staged form with 16 rows per block: 48 us at C3, 16 us for
+// one 32-token sentence).  TF >= 0: the three tables share format TF (the usual
+// case; the format switch resolves at compile time and the kernel holds only that
+// format's words: 4x the resident waves of the any-format form's 124 VGPRs).
+template <int TF>
+__device__ __forceinline__ void emb_table32(const DevTable &t, int row, int b, float (&r)[32])
+{
+    if constexpr (TF < 0) {
+        table32(t, row, b, r);
+    } else {
+        DevTable u = t;
+        u.fmt = TF;
+        table32(u, row, b, r);
+    }
+}
 
-__device__ __forceinline__ float sum16(float v)
+__device__ __forceinline__ float sum32(float v)
 {
 #pragma unroll
-    for (int o = 8; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    for (int o = 16; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
 
-__global__ __launch_bounds__(256) void embed_ln_kernel(DevTable word, DevTable type, DevTable pos,
+// resident waves per SIMD the register budget is held to (no spills at these)
+constexpr int emb_occ(int tf) { return tf == FMT_Q4_0 || tf == FMT_F16 ? 8 : tf < 0 ? 4 : 6; }
+
+template <int TF>
+__global__ __launch_bounds__(256, emb_occ(TF)) void embed_ln_kernel(DevTable word, DevTable type, DevTable pos,
                                                        const float *__restrict__ ln_w, const int32_t *__restrict__ ids,
                                                        const int32_t *__restrict__ cu, int d, h16 *__restrict__ z,
                                                        float2 *__restrict__ stats)
 {
-    // the block's 16 rows pos + (type[0] + word[id]) (bert.cpp:968-973 operand
-    // order, f32) staged in LDS by whole quant blocks -- (row, 32-column block)
-    // items over the 256 threads, a few wide loads each instead of three narrow
-    // loads per 4 values -- then read back by the row groups below
-    extern __shared__ __attribute__((aligned(16))) float vs[];   // [16][d]
-    const int b = blockIdx.y, l16 = threadIdx.x & 15;
+    const int b = blockIdx.y, l32 = threadIdx.x & 31;
     const int start = cu[b], len = cu[b + 1] - start;
-    {
-        const int nb = d / 32;
-        for (int it = threadIdx.x; it < 16 * nb; it += 256) {
-            const int r = it / nb, k = it - r * nb, ii = blockIdx.x * 16 + r;
-            float v[32];
-            if (ii < len) {
-                float w[32], ty[32], p[32];
-                table32(word, ids[start + ii], k, w);
-                table32(type, 0, k, ty);
-                table32(pos, ii, k, p);
-#pragma unroll
-                for (int e = 0; e < 32; ++e) v[e] = p[e] + (ty[e] + w[e]);
-            } else {
-#pragma unroll
-                for (int e = 0; e < 32; ++e) v[e] = 0.f;   // rows past the sentence: never stored
-            }
-            f32x4 *dst = (f32x4 *)(vs + r * d + 32 * k);
-#pragma unroll
-            for (int q = 0; q < 8; ++q) dst[q] = f32x4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
-        }
-        __syncthreads();
-    }
-    const int i = blockIdx.x * 16 + (threadIdx.x >> 4);
-    const bool ok = i < len;                       // whole 16-lane groups: the shuffles stay in-group
-    const int t = start + (ok ? i : 0);
-    const float *vrow = vs + (threadIdx.x >> 4) * d;
-    const int ns = d / 64;
-    f32x4 v[EMB_MAXS];
+    const int i = blockIdx.x * 8 + (threadIdx.x >> 5);
+    if (i >= len) return;                          // whole 32-lane groups: the shuffles stay in-group
+    const int t = start + i;
+    const bool act = l32 < d / 32;
+    float v[32];
     float s = 0.f;
+    if (act) {
+        // pos + (type[0] + word[id]) in the reference's operand order (bert.cpp:968-973), f32
+        // (one table at a time into a 32-value temporary: 64 live values, not 128)
+        float tmp[32];
+        emb_table32<TF>(word, ids[t], l32, v);
+        emb_table32<TF>(type, 0, l32, tmp);
 #pragma unroll
-    for (int k = 0; k < EMB_MAXS; ++k) {
-        if (k < ns) {
-            const int c = 4 * (l16 + 16 * k);
-            v[k] = *(const f32x4 *)(vrow + c);
-            s += (v[k][0] + v[k][1]) + (v[k][2] + v[k][3]);
-        }
+        for (int e = 0; e < 32; ++e) v[e] = tmp[e] + v[e];
+        emb_table32<TF>(pos, i, l32, tmp);
+#pragma unroll
+        for (int e = 0; e < 32; ++e) v[e] = tmp[e] + v[e];
+#pragma unroll
+        for (int e = 0; e < 32; e += 4) s += (v[e] + v[e + 1]) + (v[e + 2] + v[e + 3]);
     }
     // ggml_norm (eps 1e-5, mean then centred variance; bert.cpp:977-984) of the f32 row
-    const float mean = sum16(s) / (float)d;
+    const float mean = sum32(s) / (float)d;
     float s2 = 0.f;
+    if (act) {
 #pragma unroll
-    for (int k = 0; k < EMB_MAXS; ++k) {
-        if (k < ns) {
+        for (int e = 0; e < 32; ++e) { const float u = v[e] - mean; s2 += u * u; }
+    }
+    const float r = 1.0f / sqrtf(sum32(s2) / (float)d + 1e-5f);
+    if (act) {
+        const f32x4 *g4 = (const f32x4 *)(ln_w + 32 * l32);
+        h16x8 *dst = (h16x8 *)(z + (size_t)t * d + 32 * l32);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) { const float u = v[k][e] - mean; s2 += u * u; }
+        for (int q = 0; q < 4; ++q) {
+            const f32x4 g0 = g4[2 * q], g1 = g4[2 * q + 1];
+            h16x8 zh;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                zh[e] = (h16)(v[8 * q + e] * g0[e]);
+                zh[4 + e] = (h16)(v[8 * q + 4 + e] * g1[e]);
+            }
+            dst[q] = zh;                            // the stream as z = y * gamma (kernels.h LN fold)
         }
     }
-    const float r = 1.0f / sqrtf(sum16(s2) / (float)d + 1e-5f);
-    if (!ok) return;
-#pragma unroll
-    for (int k = 0; k < EMB_MAXS; ++k) {
-        if (k < ns) {
-            const int c = 4 * (l16 + 16 * k);
-            const f32x4 g = *(const f32x4 *)(ln_w + c);
-            h16x4 zh;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) zh[e] = (h16)(v[k][e] * g[e]);
-            *(h16x4 *)(z + (size_t)t * d + c) = zh;   // the stream as z = y * gamma (kernels.h LN fold)
-        }
-    }
-    if (l16 == 0) stats[t] = float2{mean, r};
+    if (l32 == 0) stats[t] = float2{mean, r};
 }
 
 // Row statistics from the residual GEMM's 32-feature group partials (sum, M2 about
@@ -276,8 +273,18 @@ void launch_embed_ln(const DevTable &word, const DevTable &type, const DevTable 
                      const int32_t *ids, const int32_t *cu, int32_t n_seqs, int32_t max_len, int32_t d, uint16_t *z,
                      float2 *stats, hipStream_t s)
 {
-    dim3 grid((max_len + 15) / 16, n_seqs);
-    embed_ln_kernel<<<grid, 256, (size_t)16 * d * 4, s>>>(word, type, pos, ln_w, ids, cu, d, (h16 *)z, stats);
+    dim3 grid((max_len + 7) / 8, n_seqs);
+    const int f = word.fmt == type.fmt && word.fmt == pos.fmt ? word.fmt : -1;
+#define EMB_LAUNCH(TF) embed_ln_kernel<TF><<<grid, 256, 0, s>>>(word, type, pos, ln_w, ids, cu, d, (h16 *)z, stats)
+    switch (f) {
+    case FMT_F32: EMB_LAUNCH(FMT_F32); break;
+    case FMT_F16: EMB_LAUNCH(FMT_F16); break;
+    case FMT_Q4_0: EMB_LAUNCH(FMT_Q4_0); break;
+    case FMT_Q4_1: EMB_LAUNCH(FMT_Q4_1); break;
+    case FMT_Q8_0: EMB_LAUNCH(FMT_Q8_0); break;
+    default: EMB_LAUNCH(-1); break;
+    }
+#undef EMB_LAUNCH
 }
 
 int launch_ln_stats(const float2 *part, int32_t G, int32_t stride, int32_t rows, int32_t d, float2 *stats,
