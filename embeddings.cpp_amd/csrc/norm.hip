@@ -137,6 +137,7 @@ constexpr int POOL_CHUNK = 64;
 // of every TT-th token of the chunk: column group t % G (G = d / 8 <= 128),
 // token lane t / G; the token lanes are summed through LDS in a fixed order,
 // the result in (s0, s1) of threads t < G (columns 8t .. 8t + 7).
+template <int UNR>
 __device__ __forceinline__ void pool_chunk_sum(const h16 *__restrict__ z, const float2 *__restrict__ stats,
                                                const float *__restrict__ lw, const float *__restrict__ lb,
                                                const int32_t *__restrict__ cu, int d, int b, int ch, f32x4 &s0,
@@ -153,7 +154,7 @@ __device__ __forceinline__ void pool_chunk_sum(const h16 *__restrict__ z, const 
         const int c = 8 * cg;
         const f32x4 w0 = *(const f32x4 *)(lw + c), w1 = *(const f32x4 *)(lw + c + 4);
         const f32x4 b0 = *(const f32x4 *)(lb + c), b1 = *(const f32x4 *)(lb + c + 4);
-#pragma unroll 4
+#pragma unroll UNR
         for (int i = i0 + tl; i < i1; i += TT) {
             const h16x8 y = *(const h16x8 *)(z + (size_t)(start + i) * d + c);
             const float2 st = stats[start + i];
@@ -181,6 +182,7 @@ __device__ __forceinline__ void pool_chunk_sum(const h16 *__restrict__ z, const 
 
 // Sum the n_chunks column-sum rows of one sentence (part[k * d + c]) and
 // divide by the L2 norm (bert.cpp:1092-1095).
+template <bool HOIST>
 __device__ __forceinline__ void pool_normalize(const float *part, int d, int n_chunks, float *__restrict__ out)
 {
     __shared__ float red[4];
@@ -190,7 +192,20 @@ __device__ __forceinline__ void pool_normalize(const float *part, int d, int n_c
     int ne = 0;
     for (int c = tid; c < d; c += 256) {
         float v = 0.f;
-        for (int k = 0; k < n_chunks; ++k) v += part[(size_t)k * d + c];
+        if constexpr (HOIST) {
+            // global partials: the first 16 chunks' values loaded before the first
+            // add (the serial load-add loop was 8 us at C3), summed in chunk order
+            float pv[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if (k < n_chunks) pv[k] = part[(size_t)k * d + c];
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if (k < n_chunks) v += pv[k];
+            for (int k = 16; k < n_chunks; ++k) v += part[(size_t)k * d + c];
+        } else {
+            for (int k = 0; k < n_chunks; ++k) v += part[(size_t)k * d + c];
+        }
         e[ne++] = v;
         ss += v * v;
     }
@@ -211,7 +226,7 @@ __global__ __launch_bounds__(256) void pool_partial_kernel(const h16 *__restrict
 {
     const int b = blockIdx.y, ch = blockIdx.x, tid = threadIdx.x;
     f32x4 s0, s1;
-    pool_chunk_sum(z, stats, lw, lb, cu, d, b, ch, s0, s1);
+    pool_chunk_sum<8>(z, stats, lw, lb, cu, d, b, ch, s0, s1);   // 32 tokens per thread at L 512
     if (tid < d / 8) {
         float *dst = part + ((size_t)b * n_chunks + ch) * d + 8 * tid;
         *(f32x4 *)dst = s0;
@@ -224,7 +239,7 @@ __global__ __launch_bounds__(256) void pool_final_kernel(const float *__restrict
                                                          float *__restrict__ out)
 {
     const int b = blockIdx.x;
-    pool_normalize(part + (size_t)b * n_chunks * d, d, n_chunks, out + (size_t)b * d);
+    pool_normalize<true>(part + (size_t)b * n_chunks * d, d, n_chunks, out + (size_t)b * d);
 }
 
 // Batches of at most POOL_ONE_MAX chunks (max_len <= 256): both stages in one
@@ -241,14 +256,14 @@ __global__ __launch_bounds__(256) void pool_one_kernel(const h16 *__restrict__ z
     const int b = blockIdx.x, tid = threadIdx.x;
     for (int ch = 0; ch < n_chunks; ++ch) {
         f32x4 s0, s1;
-        pool_chunk_sum(z, stats, lw, lb, cu, d, b, ch, s0, s1);
+        pool_chunk_sum<4>(z, stats, lw, lb, cu, d, b, ch, s0, s1);
         if (tid < d / 8) {
             *(f32x4 *)(cs + ch * d + 8 * tid) = s0;
             *(f32x4 *)(cs + ch * d + 8 * tid + 4) = s1;
         }
         __syncthreads();   // pool_chunk_sum's reduction buffer is reused by the next chunk
     }
-    pool_normalize(cs, d, n_chunks, out + (size_t)b * d);
+    pool_normalize<false>(cs, d, n_chunks, out + (size_t)b * d);
 }
 
 // diagnostics (BERT_CHECK_FINITE): count non-finite values of a buffer
