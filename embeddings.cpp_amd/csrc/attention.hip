@@ -392,7 +392,6 @@ extern "C" __attribute__((visibility("default"))) int bertx_att_stamps(unsigned 
 #define ASTAMP(k, v) do { } while (0)
 #endif
 
-template <bool LATE_STORE>
 __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restrict__ qkv,
                                                               const int32_t *__restrict__ cu, int d, int nh,
                                                               int n_items, float sl2, h16 *__restrict__ out)
@@ -646,15 +645,14 @@ __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restr
             }
         }
         ASTAMP(4, __builtin_amdgcn_s_memtime());
-        // LATE_STORE (production): the item's rows are stored after the S barrier.
-        // !LATE_STORE stores them BEFORE S, so a wave that finishes early writes
-        // while the slower ones still compute; measured 2 us slower (the early
-        // stores queue behind / in front of the next item's region-A pieces).  The stores
-        // are bounds-checked buffer stores on every lane of an active wave (rows
-        // past the sentence fall outside the resource and are dropped), so an
-        // active wave issues exactly ATT_NST of them and the wait in front of S
-        // is exact: the next item's Q (4 loads) and the stores stay in flight,
-        // every older piece (the next item's region A) is retired.
+        // The item's rows are stored after the S barrier (storing them before S,
+        // so a wave that finishes early writes while the slower ones still
+        // compute, measured 2 us slower: the early stores queue in front of the
+        // next item's region-A pieces, profiles/r03_attention_store_ab.log).  The
+        // stores are bounds-checked buffer stores on every lane of an active wave
+        // (rows past the sentence fall outside the resource and are dropped).  The
+        // wait in front of S is exact: the next item's Q (4 loads) stays in
+        // flight, every older piece (the next item's region A) is retired.
         if (more) load_q(nx);
         auto store_rows = [&]() {
             // lane (q, hi) holds dh 8m + 4 hi .. +3 of chunks m = 4t + g; one
@@ -695,18 +693,12 @@ __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restr
             }
         };
         static_assert(DH / 16 == 4, "four stores per active wave");
-        if (!LATE_STORE && active) {
-            store_rows();
-            if (more) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // 4 Q loads + 4 stores younger
-            else wait_all_vm();
-        } else {
-            if (more) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // the 4 Q loads younger
-            else wait_all_vm();
-        }
+        if (more) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // the 4 Q loads younger
+        else wait_all_vm();
         ASTAMP(5, __builtin_amdgcn_s_memtime());
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // no LDS read in flight into the store phase
         __syncthreads();                                  // S: region B is free
-        if (LATE_STORE && active) store_rows();           // production: all waves store after S
+        if (active) store_rows();
         ASTAMP(6, __builtin_amdgcn_s_memtime());
 #ifdef ATT_STAMPS
         ASTAMP(7, (unsigned long long)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11)));
@@ -735,17 +727,8 @@ void launch_attention(const uint16_t *qkv, const int32_t *cu, int32_t n_seqs, in
             const int n_items = n_seqs * n_head;
             const int cap = g_att_variant == 7 ? 7 : device_cu_count();
             const int grid = n_items < cap ? n_items : cap;
-            // stores after the S barrier (default); BERT_ATT_EARLY_STORE=1 stores
-            // before it -- measured 2 us slower at C3 (70.3 vs 72.6 us,
-            // profiles/r03_attention_store_ab.log): the early stores compete with
-            // the next item's region-A loads the waves are still waiting for
-            static const bool late = [] { const char *e = std::getenv("BERT_ATT_EARLY_STORE"); return !(e && *e == '1'); }();
-            if (grid > 0) {
-                if (late)
-                    attention_lds3_kernel<true><<<grid, 1024, 0, s>>>((const h16 *)qkv, cu, d, n_head, n_items, sl2, (h16 *)out);
-                else
-                    attention_lds3_kernel<false><<<grid, 1024, 0, s>>>((const h16 *)qkv, cu, d, n_head, n_items, sl2, (h16 *)out);
-            }
+            if (grid > 0)
+                attention_lds3_kernel<<<grid, 1024, 0, s>>>((const h16 *)qkv, cu, d, n_head, n_items, sl2, (h16 *)out);
         } else {
             attention_lds_kernel<32><<<g, blk, 0, s>>>((const h16 *)qkv, cu, d, n_head, sl2, (h16 *)out);
         }
