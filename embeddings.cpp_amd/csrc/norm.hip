@@ -105,10 +105,21 @@ __global__ __launch_bounds__(256, emb_occ(TF)) void embed_ln_kernel(DevTable wor
 // et al.).  One thread per row, its G partials loaded at once (G <= 32, unrolled:
 // every load in flight before the first add), 64-row blocks so short batches still
 // spread over the CUs; reads part[g][rows] coalesced along the rows.
+// Row block of workgroup b, XCD-aware: workgroups are dealt to the 8 XCDs round
+// robin, and XCD x takes the x-th eighth of the row blocks -- the rows whose
+// partials the residual GEMM's tiles on XCD x just wrote (gemm.hip remaps its
+// tiles the same way, panel-major), and whose statistics the next GEMM's tiles
+// on XCD x read: both stay in that XCD's L2.
+__device__ __forceinline__ int xcd_block(int b, int nb)
+{
+    const int xcd = b & 7, qq = nb >> 3, rr = nb & 7;
+    return (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
+}
+
 __global__ __launch_bounds__(64) void ln_stats_any(const float2 *__restrict__ part, int G, int stride, int rows,
                                                    int d, float2 *__restrict__ stats)
 {
-    const int t = blockIdx.x * 64 + threadIdx.x;
+    const int t = xcd_block(blockIdx.x, gridDim.x) * 64 + threadIdx.x;
     if (t >= rows) return;
     float2 p[32];
 #pragma unroll
@@ -121,7 +132,7 @@ template <int G>
 __global__ __launch_bounds__(64) void ln_stats_kernel(const float2 *__restrict__ part, int stride, int rows, int d,
                                                       float2 *__restrict__ stats)
 {
-    const int t = blockIdx.x * 64 + threadIdx.x;
+    const int t = xcd_block(blockIdx.x, gridDim.x) * 64 + threadIdx.x;
     if (t >= rows) return;
     float2 p[G];
 #pragma unroll
