@@ -84,6 +84,11 @@ def load_lib(path=None):
     L.bertx_test_gemm.argtypes = [c_i32, c_i32, c_i32, vp, c_f32p, c_i32, vp, c_i32, vp, vp, c_i32]
     L.bertx_test_gemm_ln.restype = c_i32
     L.bertx_test_gemm_ln.argtypes = [c_i32, c_i32, c_i32, vp, vp, c_i32, vp, vp, vp, vp, c_i32] + [vp] * 7 + [c_i32]
+    try:   # (absent from libraries built before it: BERT_LIB A/B runs against older builds)
+        L.bertx_test_gemm_fold.restype = c_i32
+        L.bertx_test_gemm_fold.argtypes = [c_i32, c_i32, c_i32, vp, vp, c_i32, vp, vp, vp, vp, c_i32, vp, vp, vp, c_i32]
+    except AttributeError:
+        pass
     L.bertx_test_gemm_ran.restype = c_i32
     L.bertx_test_gemm_ran.argtypes = []
     L.bertx_test_gemm_f32.restype = c_i32

@@ -605,15 +605,29 @@ int Device::launch_all(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, in
     // projection, st_ its (mean, 1/sigma) (kernels.h LN fold); (gz, bz) is that LN
     const float *gz = ln_e_w_, *bz = ln_e_b_;
     const int G = d / 32;
+    // Small batches: the projections combine their input's LN statistics from the
+    // residual GEMM's partials themselves (LnFold::in_part; the column-0 tiles store
+    // them for the residual GEMM after), so only the last ln_stats launch (for the
+    // pool) remains: 2 n_layer - 1 fewer launches, the same bits (the combine is
+    // ln_stats_kernel's arithmetic).  Where the tile config has no LDS for it (the
+    // large-batch tiles, d > 768 on 64-row tiles), the statistics launches stay.
+    static const bool fold_env = [] { const char *e = std::getenv("BERT_STATS_FOLD"); return !(e && *e == '0'); }();
+    const bool fold = fold_env && !layers_.empty() && gemm_fold_ok(layers_[0].qkv, M, G) && gemm_fold_ok(layers_[0].up, M, G);
 
     const double att_flop = att_flop_;   // sum over sentences of 4 d len^2 (QK^T and PV), set by the caller
     for (int l = 0; l < hp_.n_layer; ++l) {
         const DevLayer &L = layers_[(size_t)l];
         LnFold in;
-        in.in_stats = st_;
+        if (fold && l > 0) {
+            // the stream of the previous FFN-down: its partials; the rows' statistics
+            // go to st_ for this layer's O-proj residual
+            in.in_part = part_; in.in_part_stride = (int32_t)rows_; in.in_G = G; in.st_out = st_;
+        } else {
+            in.in_stats = st_;
+        }
         in.c1 = L.c1_qkv;
         begin(K_GEMM_QKV, s, ev);
-        launch_gemm(L.qkv, z_, M, L.c2_qkv, EPI_BIAS_F16, nullptr, qkv_, s, in);
+        if (launch_gemm(L.qkv, z_, M, L.c2_qkv, EPI_BIAS_F16, nullptr, qkv_, s, in) != 0) return -1;
         end(K_GEMM_QKV, s, ev, 2.0 * t * 3.0 * d * d);
         chk("gemm_qkv", l, qkv_, (size_t)T * 3 * d, 1);
 
@@ -631,14 +645,20 @@ int Device::launch_all(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, in
         end(K_GEMM_O, s, ev, 2.0 * t * d * d);
         chk("gemm_o", l, z_, (size_t)T * d, 1);
 
-        begin(K_LN_STATS, s, ev);
-        if (launch_ln_stats(part_, G, (int32_t)rows_, M, d, st_, s) != 0) return -1;
-        end(K_LN_STATS, s, ev, (double)M * (G + 1) * 8.0);
+        if (!fold) {
+            begin(K_LN_STATS, s, ev);
+            if (launch_ln_stats(part_, G, (int32_t)rows_, M, d, st_, s) != 0) return -1;
+            end(K_LN_STATS, s, ev, (double)M * (G + 1) * 8.0);
+        }
         gz = L.ln1_w; bz = L.ln1_b;
 
+        if (fold) {
+            in.in_stats = nullptr;
+            in.in_part = part_; in.in_part_stride = (int32_t)rows_; in.in_G = G; in.st_out = st_;
+        }
         in.c1 = L.c1_up;
         begin(K_GEMM_FFN_UP, s, ev);
-        launch_gemm(L.up, z_, M, L.c2_up, EPI_BIAS_GELU_F16, nullptr, ffn_, s, in);
+        if (launch_gemm(L.up, z_, M, L.c2_up, EPI_BIAS_GELU_F16, nullptr, ffn_, s, in) != 0) return -1;
         end(K_GEMM_FFN_UP, s, ev, 2.0 * t * d * f);
         chk("gemm_up", l, ffn_, (size_t)T * f, 1);
 
@@ -650,9 +670,11 @@ int Device::launch_all(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, in
         end(K_GEMM_FFN_DOWN, s, ev, 2.0 * t * d * f);
         chk("gemm_down", l, z_, (size_t)T * d, 1);
 
-        begin(K_LN_STATS, s, ev);
-        if (launch_ln_stats(part_, G, (int32_t)rows_, M, d, st_, s) != 0) return -1;
-        end(K_LN_STATS, s, ev, (double)M * (G + 1) * 8.0);
+        if (!fold || l + 1 == hp_.n_layer) {   // (fold: only the pool's statistics)
+            begin(K_LN_STATS, s, ev);
+            if (launch_ln_stats(part_, G, (int32_t)rows_, M, d, st_, s) != 0) return -1;
+            end(K_LN_STATS, s, ev, (double)M * (G + 1) * 8.0);
+        }
         gz = L.ln2_w; bz = L.ln2_b;
     }
     begin(K_POOL_L2, s, ev);
@@ -807,6 +829,60 @@ extern "C" int32_t bertx_test_gemm(int32_t fmt, int32_t N, int32_t K, const void
 {
     return bertx_test_gemm_ln(fmt, N, K, w_rows, bias, M, x, nullptr, nullptr, nullptr, epi, (const uint16_t *)res,
                               nullptr, nullptr, nullptr, nullptr, (uint16_t *)out, nullptr, cfg);
+}
+
+extern "C" int32_t bertx_test_gemm_fold(int32_t fmt, int32_t N, int32_t K, const void *w_rows, const float *bias,
+                                        int32_t M, const uint16_t *x, const float *part, const float *in_g,
+                                        const float *in_b, int32_t epi, uint16_t *out, float *st_out,
+                                        float *st_kernel, int32_t cfg)
+{
+    using namespace emb;
+    if (!fmt_valid(fmt) || K % 64 || N % 32 || M <= 0 || (epi != 0 && epi != 1) || !part || !in_g || !in_b ||
+        hip_device_count() == 0)
+        return -1;
+    const int Mp = (int)align_up((size_t)M, GEMM_BM), G = (fmt == FMT_F32 ? K : K) / 32;
+    DeviceGuard guard(0);
+    HIP_RC(guard.status());
+    HookBufs B;
+    HostTensor t;
+    DevWeight W;
+    if (!hook_weight(fmt, N, K, w_rows, t, W, B)) return -1;
+    g_gemm_cfg = cfg;
+    const bool ok = gemm_fold_ok(W, Mp, G);
+    g_gemm_cfg = 0;
+    if (!ok) return -2;
+    const HostTensor hb = vec_tensor(bias, N), hg = vec_tensor(in_g, K), hbt = vec_tensor(in_b, K);
+    Piece c1, c2;
+    fold_ln({&t}, {&hb}, hg, hbt, c1, c2, fmt == FMT_F32);
+    LnFold ln;
+    // partials [G][M] on the host -> [G][Mp] on the device (stride Mp)
+    std::vector<float> hp((size_t)G * Mp * 2, 0.f);
+    for (int g = 0; g < G; ++g) std::memcpy(&hp[(size_t)g * Mp * 2], part + (size_t)g * M * 2, (size_t)M * 8);
+    ln.in_part = (const float2 *)B.up(hp.data(), hp.size() * 4, 0);
+    ln.in_part_stride = Mp;
+    ln.in_G = G;
+    ln.st_out = (float2 *)B.up(nullptr, 0, (size_t)Mp * 8);
+    ln.c1 = (const float *)B.up(c1.bytes.data(), c1.bytes.size(), 0);
+    const float *dbias = (const float *)B.up(c2.bytes.data(), c2.bytes.size(), 0);
+    void *dx = B.up(x, (size_t)M * K * 2, (size_t)Mp * K * 2);
+    void *dout = B.up(nullptr, 0, (size_t)Mp * N * 2);
+    if (B.bad) return -1;
+    g_gemm_cfg = cfg;
+    const int rc = launch_gemm(W, (const uint16_t *)dx, Mp, dbias, epi, nullptr, dout, nullptr, ln);
+    g_gemm_cfg = 0;
+    if (rc != 0) return rc;
+    HIP_RC(hipGetLastError());
+    HIP_RC(hipDeviceSynchronize());
+    HIP_RC(hipMemcpy(out, dout, (size_t)M * N * 2, hipMemcpyDeviceToHost));
+    if (st_out) HIP_RC(hipMemcpy(st_out, ln.st_out, (size_t)M * 8, hipMemcpyDeviceToHost));
+    if (st_kernel) {
+        // the same partials through the statistics kernel (the launch form)
+        float2 *dk = (float2 *)B.up(nullptr, 0, (size_t)Mp * 8);
+        if (B.bad || launch_ln_stats(ln.in_part, G, Mp, Mp, 32 * G, dk, nullptr) != 0) return -1;
+        HIP_RC(hipDeviceSynchronize());
+        HIP_RC(hipMemcpy(st_kernel, dk, (size_t)M * 8, hipMemcpyDeviceToHost));
+    }
+    return 0;
 }
 
 extern "C" int32_t bertx_test_gemm_ln(int32_t fmt, int32_t N, int32_t K, const void *w_rows, const float *bias,

@@ -163,10 +163,12 @@ constexpr int zepi_arrays()
     return EPI == EPI_BIAS_RES ? (LNF ? 4 : 1) : (LNF ? 2 : 1);
 }
 constexpr int zkib(int bytes) { return (bytes + 1023) / 1024; }
-template <int EPI, bool LNF, int BN, int BM>
+template <int EPI, bool LNF, int BN, int BM, int GF = 0>
 constexpr int zepi_lds()
 {
-    return 1024 * (zkib(zepi_arrays<EPI, LNF>() * BN * 4) + (LNF ? zkib(BM * 8) : 0));
+    // GF > 0 (statistics fold): + the partials of up to GF 32-feature groups of the
+    // tile's BM rows, [group][row] float2
+    return 1024 * (zkib(zepi_arrays<EPI, LNF>() * BN * 4) + (LNF ? zkib(BM * 8) : 0) + zkib(GF * BM * 8));
 }
 
 // vmcnt accounting of the K loop, derived instead of hand-counted.  Each wave
@@ -255,7 +257,7 @@ static_assert(z_waits<4, 4, 2, 4>().front == 3 * 6 && z_waits<4, 4, 2, 4>().back
 // The tile body: workgroup b of a grid of nTiles tiles (nN column tiles),
 // staging X in `smem` (NS * BM * 128 B of LDS) and the epilogue operands
 // behind it (zepi_lds).
-template <int FMT, int EPI, bool LNF, int NW, int BM, int NS, int FA, int WR, int NT, int XI>
+template <int FMT, int EPI, bool LNF, int NW, int BM, int NS, int FA, int WR, int NT, int XI, int GF>
 __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b, DevWeight W,
                                            const h16 *__restrict__ X, const float *__restrict__ bias,
                                            const void *__restrict__ res, void *__restrict__ out, int nN, int nTiles,
@@ -357,6 +359,29 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     float *const efeat = (float *)(smem + RING);
     float2 *const estat = (float2 *)(smem + RING + FP * 1024);
     const float2 *stp = RES ? ln.res_stats : ln.in_stats;
+    // Statistics fold (GF > 0; small batches, engine.cpp): instead of the rows'
+    // (mean, 1/sigma), the residual GEMM's 32-feature partials of the tile's rows
+    // come in with the prologue (one load latency, beside X(0) and W(0)) and are
+    // combined after the K loop with ln_stats_kernel's arithmetic -- no statistics
+    // launch in front of this GEMM, same bits.
+    constexpr bool FOLD = GF > 0;
+    static_assert(!FOLD || (LNF && !RES && BM % 64 == 0), "fold: input-LN forms");
+    float2 *const epart = (float2 *)(smem + RING + (FP + SP) * 1024);
+    if constexpr (FOLD) {
+        if (wave == 1 % NW) {
+            // piece j, lane l: elements e = 128 j + 2 l, + 1 of [group][row] (BM rows per
+            // group); one wave issues them all (spread over every wave, each wave's
+            // K loop started later: B = 1 +2 us, profiles/r04_stats_fold_ab.log)
+            const int G = ln.in_G, npc = (G * BM + 127) / 128;
+#pragma unroll
+            for (int j = 0; j < GF * BM / 128; ++j) {
+                if (j < npc) {
+                    const int e = 128 * j + 2 * lane, gg = min(e / BM, G - 1), r = e % BM;
+                    glds<16>(ln.in_part + (size_t)gg * ln.in_part_stride + m0 + r, (char *)epart + j * 1024);
+                }
+            }
+        }
+    }
     if (wave == 0) {
         const float *arr[4] = {bias, RES ? ln.res_g : ln.c1, ln.res_b, ln.g_next};
 #pragma unroll
@@ -364,10 +389,12 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
             const int f = 256 * i + 4 * lane, ai = f / BN < NA ? f / BN : 0;
             glds<16>(arr[ai] + min(n0 + f % BN, N - 4), (char *)efeat + i * 1024);
         }
+        if constexpr (!FOLD) {
 #pragma unroll
-        for (int i = 0; i < SP; ++i) {
-            const int r = 128 * i + 2 * lane;
-            glds<16>(stp + m0 + (r < BM ? r : 0), (char *)estat + i * 1024);
+            for (int i = 0; i < SP; ++i) {
+                const int r = 128 * i + 2 * lane;
+                glds<16>(stp + m0 + (r < BM ? r : 0), (char *)estat + i * 1024);
+            }
         }
     }
 
@@ -419,7 +446,7 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     // on every path.
     // A tail step (the remainder after the whole WR-tuples) loads no weights it
     // will use: ztail_dma stands in for them, so the counts hold.
-    const uint32_t scratch = lds_u32(smem + RING + zepi_lds<EPI, LNF, BN, BM>());
+    const uint32_t scratch = lds_u32(smem + RING + zepi_lds<EPI, LNF, BN, BM, GF>());
     auto wload_or_tail = [&](ZSet<FMT, FA> &nxt, int kw, auto tail) {
         if constexpr (decltype(tail)::value) ztail_dma<LQ>(wq + kw * qstep, scratch);
         else wload(nxt, kw);
@@ -537,6 +564,37 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     // shipped code objects for this wait).
     wait_vmcnt<0>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if constexpr (FOLD) {
+        // row tid's statistics from its G partials (ln_row_stats: the statistics
+        // kernel's arithmetic and order), into estat; the column-0 tiles also store
+        // them for the residual GEMM that reads this stream next (LnFold::st_out)
+        if (tid < BM) {
+            const int G = ln.in_G;
+            // (LDS reads from asm on the 32-bit LDS address: hipcc's generic-pointer
+            // form of these loads next to ln_row_stats' division sequence fails
+            // instruction selection on gfx950 -- "operand has incorrect register class";
+            // read as 64-bit integers: a float2 tied through an asm operand came out
+            // with its halves mixed)
+            const uint32_t pa = lds_u32(epart) + 8u * tid;
+            unsigned long long pr[GF];
+#pragma unroll
+            for (int gg = 0; gg < GF; ++gg) {
+                pr[gg] = 0ull;
+                if (gg < G) asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(pr[gg]) : "v"(pa), "i"(gg * BM * 8));
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            float2 pp[GF];
+#pragma unroll
+            for (int gg = 0; gg < GF; ++gg) {   // (each value tied to after the wait)
+                asm volatile("" : "+v"(pr[gg]));
+                pp[gg] = __builtin_bit_cast(float2, pr[gg]);
+            }
+            const float2 rs = ln_row_stats<GF>(pp, G, 32 * G);
+            estat[tid] = rs;
+            if (n0 == 0 && ln.st_out) ln.st_out[m0 + tid] = rs;
+        }
+        lds_barrier();
+    }
     ZSTAMP(2, __builtin_amdgcn_s_memtime());
 #ifdef GEMM_STAMPS
     ZSTAMP(4, __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11)));
@@ -706,20 +764,20 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     }
 }
 
-template <int FMT, int EPI, bool LNF, int NW, int BM, int NS, int FA, int WR, int NT, int XI, int OCC>
+template <int FMT, int EPI, bool LNF, int NW, int BM, int NS, int FA, int WR, int NT, int XI, int OCC, int GF>
 __global__ __launch_bounds__(64 * NW, OCC * NW / 4) void gemmz_kernel(DevWeight W, const h16 *__restrict__ X,
                                                                const float *__restrict__ bias,
                                                                const void *__restrict__ res, void *__restrict__ out,
                                                                int nN, int nTiles, LnFold ln)
 {
-    __shared__ __attribute__((aligned(16))) char smem[(XI >= 3 ? NW / NT : 1) * NS * BM * ZK * 2 + zepi_lds<EPI, LNF, 32 * (NW / NT) * FA, BM>() +
+    __shared__ __attribute__((aligned(16))) char smem[(XI >= 3 ? NW / NT : 1) * NS * BM * ZK * 2 + zepi_lds<EPI, LNF, 32 * (NW / NT) * FA, BM, GF>() +
                                                       256];   // + the tail steps' scratch slot (ztail_dma)
     // a grid smaller than nTiles walks the tiles b, b + grid, ... (persistent;
     // the host only launches it so when every wave of every tile has features,
     // so no wave leaves the body early and the barrier between tiles is reached
     // by all)
     for (int b = blockIdx.x; b < nTiles; b += gridDim.x) {
-        gemmz_body<FMT, EPI, LNF, NW, BM, NS, FA, WR, NT, XI>(smem, b, W, X, bias, res, out, nN, nTiles, ln);
+        gemmz_body<FMT, EPI, LNF, NW, BM, NS, FA, WR, NT, XI, GF>(smem, b, W, X, bias, res, out, nN, nTiles, ln);
         ZSTAMP(3, __builtin_amdgcn_s_memtime());
         if (b + (int)gridDim.x < nTiles) lds_barrier();   // LDS (X ring, epilogue operands) reused
     }
@@ -727,7 +785,7 @@ __global__ __launch_bounds__(64 * NW, OCC * NW / 4) void gemmz_kernel(DevWeight 
 
 // OCC: workgroups per CU the launch bounds ask registers for (2: two co-resident
 // tiles; 3: three, at most 168 VGPRs per wave)
-template <int FMT, int NW, int BM, int NS, int FA = 1, int WR = 3, int NT = 1, int XI = 0, int OCC = 2>
+template <int FMT, int NW, int BM, int NS, int FA = 1, int WR = 3, int NT = 1, int XI = 0, int OCC = 2, int GF = 0>
 void dispatch_z(const DevWeight &W, const h16 *x, int M, const float *bias, int epi, const void *res, void *out,
                 hipStream_t s, const LnFold &ln, bool lnf)
 {
@@ -745,15 +803,19 @@ void dispatch_z(const DevWeight &W, const h16 *x, int M, const float *bias, int 
     int grid = nTiles;
     if (persist > 0 && W.N % BN == 0) grid = std::min(nTiles, persist * cus);
     auto go = [&](auto kern) { kern<<<grid, 64 * NW, 0, s>>>(W, x, bias, res, out, nN, nTiles, ln); };
-    if (epi == EPI_BIAS_F16) {
-        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_F16, true, NW, BM, NS, FA, WR, NT, XI, OCC>);
-        else go(gemmz_kernel<FMT, EPI_BIAS_F16, false, NW, BM, NS, FA, WR, NT, XI, OCC>);
+    if constexpr (GF > 0) {
+        // statistics fold: the input-LN forms only (launch_fmt checked epi / lnf)
+        if (epi == EPI_BIAS_F16) go(gemmz_kernel<FMT, EPI_BIAS_F16, true, NW, BM, NS, FA, WR, NT, XI, OCC, GF>);
+        else go(gemmz_kernel<FMT, EPI_BIAS_GELU_F16, true, NW, BM, NS, FA, WR, NT, XI, OCC, GF>);
+    } else if (epi == EPI_BIAS_F16) {
+        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_F16, true, NW, BM, NS, FA, WR, NT, XI, OCC, 0>);
+        else go(gemmz_kernel<FMT, EPI_BIAS_F16, false, NW, BM, NS, FA, WR, NT, XI, OCC, 0>);
     } else if (epi == EPI_BIAS_GELU_F16) {
-        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_GELU_F16, true, NW, BM, NS, FA, WR, NT, XI, OCC>);
-        else go(gemmz_kernel<FMT, EPI_BIAS_GELU_F16, false, NW, BM, NS, FA, WR, NT, XI, OCC>);
+        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_GELU_F16, true, NW, BM, NS, FA, WR, NT, XI, OCC, 0>);
+        else go(gemmz_kernel<FMT, EPI_BIAS_GELU_F16, false, NW, BM, NS, FA, WR, NT, XI, OCC, 0>);
     } else {
-        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_RES, true, NW, BM, NS, FA, WR, NT, XI, OCC>);
-        else go(gemmz_kernel<FMT, EPI_BIAS_RES, false, NW, BM, NS, FA, WR, NT, XI, OCC>);
+        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_RES, true, NW, BM, NS, FA, WR, NT, XI, OCC, 0>);
+        else go(gemmz_kernel<FMT, EPI_BIAS_RES, false, NW, BM, NS, FA, WR, NT, XI, OCC, 0>);
     }
 }
 
@@ -766,28 +828,54 @@ void dispatch_z(const DevWeight &W, const h16 *x, int M, const float *bias, int 
 //   16  4 waves 64 x 64, 2 along the tokens, wave-private X rings
 //                                                      small batches, < half the CUs
 // A config whose row tile does not divide M falls back to the next smaller tile.
-template <int FMT>
-int launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, int32_t epi, const void *res,
-               void *out, hipStream_t s, LnFold ln, bool lnf, int cfg)
+// The tile config a launch of N features over M rows runs (cfg 0: the heuristic),
+// after the fallbacks for tiles that do not divide M.
+int pick_cfg(int N, int M, int cfg)
 {
     if (cfg == 0) {
         // the largest tile that still gives every CU work: 256 x 128 tiles two per CU
         // (measured fastest at C3 once there are two per CU, profiles/r01_gemm16_sweep.log),
         // else 128 x 128 once there is one per CU, else 64 x 64 (small batches)
-        const long n128 = (W.N + 127) / 128, cus = device_cu_count();
+        const long n128 = (N + 127) / 128, cus = device_cu_count();
         // small batches: 64-row tiles; while they fill less than half the CUs, on 4
         // waves (2 along the tokens: every SIMD of a CU works, each wave's K-step
         // half as long; B = 1, L = 32: 632 -> 571 us) with wave-private X rings (no
         // barrier in the K loop: 582 -> 567 us, profiles/r03_gemm_private_ab.log),
         // else on 2 (C2's O-proj and FFN-down: the 4-wave forms 6-15 % slower
         // there).  Same bits either way.
-        const long n64 = (long)(M / 64) * ((W.N + 63) / 64);
+        const long n64 = (long)(M / 64) * ((N + 63) / 64);
         const int small = 2 * n64 < cus ? 16 : 4;
         cfg = (M % 256 == 0 && (M / 256) * n128 >= 2 * cus) ? 2 : (M % 128 == 0 && (M / 128) * n128 >= cus) ? 3 : small;
     }
     if ((cfg == 2 || cfg == 11) && M % 256) cfg = 3;
     if (cfg == 3 && M % 128) cfg = 4;
     if (cfg != 2 && cfg != 11 && cfg != 3 && cfg != 16) cfg = 4;
+    return cfg;
+}
+
+// Statistics-fold capacity (LnFold::in_part) of a config: the partial groups its
+// LDS holds (cfg 3 keeps two workgroups per CU with 12: d <= 384; the 64-row
+// forms with 24: d <= 768); 0 = no fold form (the 256-row large-batch tiles).
+constexpr int fold_cap(int cfg) { return cfg == 3 ? 12 : (cfg == 4 || cfg == 16) ? 24 : 0; }
+
+template <int FMT>
+int launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, int32_t epi, const void *res,
+               void *out, hipStream_t s, LnFold ln, bool lnf, int cfg)
+{
+    cfg = pick_cfg(W.N, M, cfg);
+    if (ln.in_part) {
+        // statistics fold: the caller made sure the config has the capacity
+        // (gemm_fold_ok); anything else is an error, never a silent fallback
+        if (!lnf || epi == EPI_BIAS_RES || ln.in_G <= 0 || ln.in_G > fold_cap(cfg) || 32 * ln.in_G != (W.kx ? W.kx : W.K))
+            return -1;
+        if (ln.store_nt < 0) ln.store_nt = 0;
+        switch (cfg) {
+        case 3: dispatch_z<FMT, 4, 128, 4, 1, 3, 1, 0, 2, 12>(W, x, M, bias, epi, res, out, s, ln, lnf); break;
+        case 16: dispatch_z<FMT, 4, 64, 4, 1, 3, 2, 3, 2, 24>(W, x, M, bias, epi, res, out, s, ln, lnf); break;
+        default: dispatch_z<FMT, 2, 64, 4, 1, 3, 1, 0, 2, 24>(W, x, M, bias, epi, res, out, s, ln, lnf); break;
+        }
+        return cfg;
+    }
     // Non-temporal output stores on the 256-row tiles (large batches): the output
     // streams past L2 instead of evicting the X panels the next column tiles read
     // (C3: FFN-down 143 -> 140 us, QKV -1 us, forward +0.5 % alternating on one box,
@@ -814,6 +902,19 @@ int launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, i
 
 thread_local int g_gemm_cfg = 0;
 thread_local int g_gemm_ran = 0;
+
+// the config a forward launch asks for: the calling thread's test hook, else the
+// BERT_GEMM_CFG A/B hook, else 0 (the heuristic)
+static int forward_cfg()
+{
+    static const int env_cfg = [] { const char *e = std::getenv("BERT_GEMM_CFG"); return e ? std::atoi(e) : 0; }();
+    return g_gemm_cfg ? g_gemm_cfg : env_cfg;
+}
+
+bool gemm_fold_ok(const DevWeight &W, int32_t M, int32_t G)
+{
+    return G > 0 && M > 0 && M % 64 == 0 && 32 * G == (W.kx ? W.kx : W.K) && G <= fold_cap(pick_cfg(W.N, M, forward_cfg()));
+}
 
 // CUs of the calling thread's current device, cached per ordinal (a context may
 // hold devices in different partition modes; launches size persistent grids
@@ -850,21 +951,20 @@ int launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *b
     // LN + next gamma + partials
     const bool res_ln = ln.res_stats && ln.res_g && ln.res_b && ln.g_next && ln.part;
     if (epi == EPI_BIAS_RES && !res_ln && (ln.res_stats || ln.g_next)) return -1;
-    if (epi != EPI_BIAS_RES && ln.in_stats && !ln.c1) return -1;
-    const bool lnf = epi == EPI_BIAS_RES ? res_ln : ln.in_stats != nullptr;
+    if (epi != EPI_BIAS_RES && (ln.in_stats || ln.in_part) && !ln.c1) return -1;
+    if (ln.in_stats && ln.in_part) return -1;
+    const bool lnf = epi == EPI_BIAS_RES ? res_ln : (ln.in_stats || ln.in_part);
     static const int nt_env = [] { const char *e = std::getenv("BERT_GEMM_NT"); return e ? std::atoi(e) : -1; }();
     LnFold lnx = ln;
     lnx.store_nt = nt_env;
-    // A/B hook: BERT_GEMM_CFG forces a tile config in the forward (tests/benches set g_gemm_cfg)
-    static const int env_cfg = [] { const char *e = std::getenv("BERT_GEMM_CFG"); return e ? std::atoi(e) : 0; }();
-    const int cfg = g_gemm_cfg ? g_gemm_cfg : env_cfg;
+    const int cfg = forward_cfg();
     switch (W.fmt) {
     case FMT_Q4_0: g_gemm_ran = launch_fmt<FMT_Q4_0>(W, x, M, bias, epi, res, out, s, lnx, lnf, cfg); break;
     case FMT_Q4_1: g_gemm_ran = launch_fmt<FMT_Q4_1>(W, x, M, bias, epi, res, out, s, lnx, lnf, cfg); break;
     case FMT_Q8_0: g_gemm_ran = launch_fmt<FMT_Q8_0>(W, x, M, bias, epi, res, out, s, lnx, lnf, cfg); break;
     default: g_gemm_ran = launch_fmt<FMT_F16>(W, x, M, bias, epi, res, out, s, lnx, lnf, cfg); break;
     }
-    return 0;
+    return g_gemm_ran < 0 ? -1 : 0;
 }
 
 }  // namespace emb

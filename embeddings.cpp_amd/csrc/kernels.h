@@ -72,6 +72,14 @@ struct LnFold {
     // + bias[n], where the caller passes c2 as `bias`.  Null: plain acc + bias.
     const float2 *in_stats = nullptr;
     const float *c1 = nullptr;
+    // Statistics fold (instead of in_stats; small batches): the residual GEMM's
+    // partials of the input stream, in_part[g * in_part_stride + row] for its
+    // in_G = d / 32 groups, combined by the GEMM itself (ln_stats_kernel's
+    // arithmetic); the column-0 tiles store the rows' (mean, 1/sigma) to st_out.
+    // Only where gemm_fold_ok says the chosen tile config has the LDS for it.
+    const float2 *in_part = nullptr;
+    int32_t in_part_stride = 0, in_G = 0;
+    float2 *st_out = nullptr;
     // Residual side (EPI_BIAS_RES): `res` holds z of the previous LN (res_stats,
     // gamma res_g, beta res_b), the residual being LN(y) = r z - r mean gamma +
     // beta; res_stats null: the residual as stored.  With g_next the new stream
@@ -100,6 +108,9 @@ int launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *b
 // calling thread's last launch_gemm actually dispatched (after fallbacks).
 extern thread_local int g_gemm_cfg;
 extern thread_local int g_gemm_ran;
+// Whether launch_gemm of W over M rows can take the statistics fold (LnFold::in_part)
+// for G partial groups: the tile config it will choose has the LDS for them.
+bool gemm_fold_ok(const DevWeight &W, int32_t M, int32_t G);
 
 // CU count of the calling thread's current HIP device (cached per ordinal).
 int device_cu_count();

@@ -121,6 +121,21 @@ BERT_API int32_t bertx_test_gemm_ln(int32_t fmt, int32_t N, int32_t K, const voi
                                     const float *res_g, const float *res_b, const float *g_next, uint16_t *out,
                                     float *st_out, int32_t cfg);
 
+/*
+ * The statistics-fold form of the input-LN GEMM (epi 0/1; small batches, where the
+ * forward drops the ln_stats launches): part holds the residual GEMM's partials of
+ * the input rows, float pairs [K/32][M] (sum, squared deviations from the group
+ * mean); the GEMM combines them per row with the statistics kernel's arithmetic
+ * and then runs as bertx_test_gemm_ln with those in_stats; st_out [M] (mean,
+ * 1/sigma) receives the combined statistics (the column-0 tiles' store), st_kernel
+ * [M] (if not NULL) the statistics kernel's combine of the same partials.  Returns
+ * -2 when the tile config has no fold form for this shape.
+ */
+BERT_API int32_t bertx_test_gemm_fold(int32_t fmt, int32_t N, int32_t K, const void *w_rows, const float *bias,
+                                      int32_t M, const uint16_t *x, const float *part, const float *in_g,
+                                      const float *in_b, int32_t epi, uint16_t *out, float *st_out, float *st_kernel,
+                                      int32_t cfg);
+
 /* The tile config the calling thread's last GEMM launch dispatched (after the
  * fallbacks above), so a test can assert which kernel it exercised. */
 BERT_API int32_t bertx_test_gemm_ran(void);

@@ -238,6 +238,68 @@ def test_gemm_input_ln_fold(lib, fmt, epi, N, K, M, cfg):
     assert err <= tol, (FMTS[fmt], epi, err, tol)
 
 
+def ln_row_stats_f32(part, d):
+    """ln_row_stats (device_common.h) in numpy float32, op for op (every op IEEE
+    round-to-nearest; fmaf(-32, mean, s) and fmaf(q, 1/32, m) are exact scalings
+    plus one rounding): part [G][M][2] -> [M][2] (mean, 1/sigma)."""
+    f = np.float32
+    G, M = part.shape[0], part.shape[1]
+    s = np.zeros(M, f)
+    for g in range(G):
+        s = (s + part[g, :, 0]).astype(f)
+    mean = (s / f(d)).astype(f)
+    m2 = np.zeros(M, f)
+    for g in range(G):
+        dm = (part[g, :, 0] - (f(32) * mean).astype(f)).astype(f)
+        q = (dm * dm).astype(f)
+        m2 = (m2 + ((q / f(32)).astype(f) + part[g, :, 1]).astype(f)).astype(f)
+    r = (f(1) / np.sqrt(((m2 / f(d)).astype(f) + f(1e-5)).astype(f)).astype(f)).astype(f)
+    return np.stack([mean, r], axis=1).astype(f)
+
+
+@pytest.mark.parametrize("fmt", [1, 2, 8])
+@pytest.mark.parametrize("epi", [0, 1])
+@pytest.mark.parametrize("N,K,M,cfg", [(1152, 384, 4096, 0), (1536, 384, 200, 3), (2304, 768, 32, 0),
+                                       (3072, 768, 64, 16), (768, 768, 1000, 4), (192, 64, 10, 0)])
+def test_gemm_statistics_fold(lib, fmt, epi, N, K, M, cfg):
+    """The statistics fold of the small-batch forward (LnFold::in_part): the GEMM
+    combines the residual GEMM's per-group partials itself.  Its statistics are
+    bitwise the statistics kernel's (ln_stats, the launch form) and within rounding
+    of ln_row_stats restated in numpy float32, and its output is bitwise the output
+    of the same GEMM given those statistics, for every fold config (3: 128-row
+    tiles up to d 384; 4, 16: 64-row tiles up to d 768)."""
+    rng = np.random.default_rng(fmt * 5 + epi + N + M)
+    W = rng.standard_normal((N, K)).astype(np.float32) * 0.05
+    wb, deq = weight_rows(fmt, W)
+    bias = rng.standard_normal(N).astype(np.float32) * 0.1
+    G = K // 32
+    y = (rng.standard_normal((M, K)) * 2.0 + rng.standard_normal((M, 1)) * 3.0).astype(np.float32)
+    yg = y.reshape(M, G, 32)
+    sg = yg.sum(axis=2, dtype=np.float32)
+    q = ((yg - (sg / 32)[:, :, None]) ** 2).sum(axis=2, dtype=np.float32)
+    part = np.ascontiguousarray(np.stack([sg.T, q.T], axis=2), np.float32)      # [G][M][2]
+    stats = ln_row_stats_f32(part, K)
+    g = (1.0 + rng.standard_normal(K) * 0.3).astype(np.float32)
+    be = (rng.standard_normal(K) * 0.1).astype(np.float32)
+    z = np.ascontiguousarray((y * g).astype(np.float16))
+    out = np.zeros((M, N), np.float16)
+    st = np.zeros((M, 2), np.float32)
+    stk = np.zeros((M, 2), np.float32)
+    rc = lib.bertx_test_gemm_fold(fmt, N, K, wb, f32p(bias), M, z.ctypes.data, part.ctypes.data, f32p(g), f32p(be),
+                                  epi, out.ctypes.data, st.ctypes.data, stk.ctypes.data, cfg)
+    assert rc == 0, rc
+    # bitwise the statistics kernel's combine of the same partials (the launch form)
+    assert np.array_equal(st.view(np.uint32), stk.view(np.uint32))
+    # and the restated arithmetic within the device's f32 division / square root
+    assert np.allclose(st, stats, rtol=5e-7, atol=1e-12), np.abs(st - stats).max()
+    stats = stk
+    ref = np.zeros((M, N), np.float16)
+    assert lib.bertx_test_gemm_ln(fmt, N, K, wb, f32p(bias), M, z.ctypes.data, np.ascontiguousarray(stats).ctypes.data,
+                                  f32p(g), f32p(be), epi, None, None, None, None, None, ref.ctypes.data, None,
+                                  cfg) == 0
+    assert np.array_equal(out.view(np.uint16), ref.view(np.uint16))
+
+
 @pytest.mark.parametrize("fmt", [1, 2, 3, 8])
 @pytest.mark.parametrize("N,K,M,cfg", [(768, 768, 512, 0), (384, 1536, 256, 3), (1024, 1024, 384, 2),
                                        (768, 3072, 256, 0), (384, 1536, 130, 4), (768, 3072, 384, 11),
