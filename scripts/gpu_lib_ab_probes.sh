@@ -6,7 +6,7 @@ OUT=gpurun_out/${TAG:-libabp}
 mkdir -p $OUT
 for r in $(seq 1 ${ROUNDS:-2}); do
   for lib in new old; do
-    if [ $lib = new ]; then L=build/libbert.so; else L=${OLD:-build/old}/libbert.so; fi
+    if [ $lib = new ]; then L=${NEW:-build}/libbert.so; else L=${OLD:-build/old}/libbert.so; fi
     BERT_LIB=$L timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-pmc --no-library --steps 30 > $OUT/${lib}_r$r.log 2>&1 || { tail -20 $OUT/${lib}_r$r.log; exit 1; }
     python3 -c "
 import json;l=[x for x in open('$OUT/${lib}_r$r.log') if x.startswith('{')][-1];d=json.loads(l);k=d['kernels']
