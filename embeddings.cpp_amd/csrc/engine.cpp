@@ -840,7 +840,7 @@ extern "C" int32_t bertx_test_gemm_fold(int32_t fmt, int32_t N, int32_t K, const
     if (!fmt_valid(fmt) || K % 64 || N % 32 || M <= 0 || (epi != 0 && epi != 1) || !part || !in_g || !in_b ||
         hip_device_count() == 0)
         return -1;
-    const int Mp = (int)align_up((size_t)M, GEMM_BM), G = (fmt == FMT_F32 ? K : K) / 32;
+    const int Mp = (int)align_up((size_t)M, GEMM_BM), G = K / 32;   // (X columns: K for every format)
     DeviceGuard guard(0);
     HIP_RC(guard.status());
     HookBufs B;
