@@ -166,10 +166,9 @@ constexpr int zkib(int bytes) { return (bytes + 1023) / 1024; }
 template <int EPI, bool LNF, int BN, int BM, int GF = 0>
 constexpr int zepi_lds()
 {
-    // GF > 0 (statistics fold, partials staged by the prologue): + the partials of up
-    // to GF 32-feature groups of the tile's BM rows, [group][row] float2 (GF < 0: the
-    // partials are loaded into registers after the K loop, no LDS)
-    return 1024 * (zkib(zepi_arrays<EPI, LNF>() * BN * 4) + (LNF ? zkib(BM * 8) : 0) + zkib((GF > 0 ? GF : 0) * BM * 8));
+    // GF > 0 (statistics fold): + the partials of up to GF 32-feature groups of the
+    // tile's BM rows, [group][row] float2
+    return 1024 * (zkib(zepi_arrays<EPI, LNF>() * BN * 4) + (LNF ? zkib(BM * 8) : 0) + zkib(GF * BM * 8));
 }
 
 // vmcnt accounting of the K loop, derived instead of hand-counted.  Each wave
@@ -360,19 +359,15 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     float *const efeat = (float *)(smem + RING);
     float2 *const estat = (float2 *)(smem + RING + FP * 1024);
     const float2 *stp = RES ? ln.res_stats : ln.in_stats;
-    // Statistics fold (GF != 0, engine.cpp): instead of the rows' (mean, 1/sigma),
-    // the residual GEMM's 32-feature partials of the tile's rows are combined after
-    // the K loop with ln_stats_kernel's arithmetic -- no statistics launch in front
-    // of this GEMM, same bits.  GF > 0 (64- and 128-row tiles): the partials come
-    // in with the prologue (one load latency, beside X(0) and W(0)) into LDS;
-    // GF < 0 (256-row tiles, whose LDS holds two workgroups per CU): each thread
-    // loads its row's partials into registers after the K loop (the co-resident
-    // workgroup's K loop runs under that latency).
-    constexpr bool FOLD = GF != 0;
-    constexpr int GFA = GF > 0 ? GF : -GF;
+    // Statistics fold (GF > 0; small batches, engine.cpp): instead of the rows'
+    // (mean, 1/sigma), the residual GEMM's 32-feature partials of the tile's rows
+    // come in with the prologue (one load latency, beside X(0) and W(0)) and are
+    // combined after the K loop with ln_stats_kernel's arithmetic -- no statistics
+    // launch in front of this GEMM, same bits.
+    constexpr bool FOLD = GF > 0;
     static_assert(!FOLD || (LNF && !RES && BM % 64 == 0), "fold: input-LN forms");
     float2 *const epart = (float2 *)(smem + RING + (FP + SP) * 1024);
-    if constexpr (GF > 0) {
+    if constexpr (FOLD) {
         if (wave == 1 % NW) {
             // piece j, lane l: elements e = 128 j + 2 l, + 1 of [group][row] (BM rows per
             // group); one wave issues them all (spread over every wave, each wave's
@@ -575,35 +570,26 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
         // them for the residual GEMM that reads this stream next (LnFold::st_out)
         if (tid < BM) {
             const int G = ln.in_G;
-            float2 pp[GFA];
-            if constexpr (GF > 0) {
-                // (LDS reads from asm on the 32-bit LDS address: hipcc's generic-pointer
-                // form of these loads next to ln_row_stats' division sequence fails
-                // instruction selection on gfx950 -- "operand has incorrect register class";
-                // read as 64-bit integers: a float2 tied through an asm operand came out
-                // with its halves mixed)
-                const uint32_t pa = lds_u32(epart) + 8u * tid;
-                unsigned long long pr[GFA];
+            // (LDS reads from asm on the 32-bit LDS address: hipcc's generic-pointer
+            // form of these loads next to ln_row_stats' division sequence fails
+            // instruction selection on gfx950 -- "operand has incorrect register class";
+            // read as 64-bit integers: a float2 tied through an asm operand came out
+            // with its halves mixed)
+            const uint32_t pa = lds_u32(epart) + 8u * tid;
+            unsigned long long pr[GF];
 #pragma unroll
-                for (int gg = 0; gg < GFA; ++gg) {
-                    pr[gg] = 0ull;
-                    if (gg < G) asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(pr[gg]) : "v"(pa), "i"(gg * BM * 8));
-                }
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-                for (int gg = 0; gg < GFA; ++gg) {   // (each value tied to after the wait)
-                    asm volatile("" : "+v"(pr[gg]));
-                    pp[gg] = __builtin_bit_cast(float2, pr[gg]);
-                }
-            } else {
-                // row m0 + tid's partials straight from global memory (one coalesced
-                // 8-B load per group across the wave)
-                const float2 *src = ln.in_part + m0 + tid;
-#pragma unroll
-                for (int gg = 0; gg < GFA; ++gg)   // (groups past G: loaded, unused)
-                    pp[gg] = src[(size_t)min(gg, G - 1) * ln.in_part_stride];
+            for (int gg = 0; gg < GF; ++gg) {
+                pr[gg] = 0ull;
+                if (gg < G) asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(pr[gg]) : "v"(pa), "i"(gg * BM * 8));
             }
-            const float2 rs = ln_row_stats<GFA>(pp, G, 32 * G);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            float2 pp[GF];
+#pragma unroll
+            for (int gg = 0; gg < GF; ++gg) {   // (each value tied to after the wait)
+                asm volatile("" : "+v"(pr[gg]));
+                pp[gg] = __builtin_bit_cast(float2, pr[gg]);
+            }
+            const float2 rs = ln_row_stats<GF>(pp, G, 32 * G);
             estat[tid] = rs;
             if (n0 == 0 && ln.st_out) ln.st_out[m0 + tid] = rs;
         }
@@ -817,7 +803,7 @@ void dispatch_z(const DevWeight &W, const h16 *x, int M, const float *bias, int 
     int grid = nTiles;
     if (persist > 0 && W.N % BN == 0) grid = std::min(nTiles, persist * cus);
     auto go = [&](auto kern) { kern<<<grid, 64 * NW, 0, s>>>(W, x, bias, res, out, nN, nTiles, ln); };
-    if constexpr (GF != 0) {
+    if constexpr (GF > 0) {
         // statistics fold: the input-LN forms only (launch_fmt checked epi / lnf)
         if (epi == EPI_BIAS_F16) go(gemmz_kernel<FMT, EPI_BIAS_F16, true, NW, BM, NS, FA, WR, NT, XI, OCC, GF>);
         else go(gemmz_kernel<FMT, EPI_BIAS_GELU_F16, true, NW, BM, NS, FA, WR, NT, XI, OCC, GF>);
@@ -867,15 +853,10 @@ int pick_cfg(int N, int M, int cfg)
     return cfg;
 }
 
-// Statistics-fold capacity (LnFold::in_part) of a config: the partial groups it
-// combines (cfg 3 keeps two workgroups per CU with 12 in LDS: d <= 384; the 64-row
-// forms 24 in LDS: d <= 768; the 256-row tiles 24 in registers after the K loop,
-// q4_0 only: its fold form has the register allocation of the launch form, the
-// other formats' fold forms spill 44-52 B); 0 = no fold form.
-constexpr int fold_cap(int cfg, int fmt)
-{
-    return cfg == 3 ? 12 : (cfg == 4 || cfg == 16 || (cfg == 2 && fmt == FMT_Q4_0)) ? 24 : 0;
-}
+// Statistics-fold capacity (LnFold::in_part) of a config: the partial groups its
+// LDS holds (cfg 3 keeps two workgroups per CU with 12: d <= 384; the 64-row
+// forms with 24: d <= 768); 0 = no fold form (the 256-row large-batch tiles).
+constexpr int fold_cap(int cfg) { return cfg == 3 ? 12 : (cfg == 4 || cfg == 16) ? 24 : 0; }
 
 template <int FMT>
 int launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, int32_t epi, const void *res,
@@ -885,13 +866,10 @@ int launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, i
     if (ln.in_part) {
         // statistics fold: the caller made sure the config has the capacity
         // (gemm_fold_ok); anything else is an error, never a silent fallback
-        if (!lnf || epi == EPI_BIAS_RES || ln.in_G <= 0 || ln.in_G > fold_cap(cfg, FMT) || 32 * ln.in_G != (W.kx ? W.kx : W.K))
+        if (!lnf || epi == EPI_BIAS_RES || ln.in_G <= 0 || ln.in_G > fold_cap(cfg) || 32 * ln.in_G != (W.kx ? W.kx : W.K))
             return -1;
-        if (ln.store_nt < 0) ln.store_nt = cfg == 2 ? 1 : 0;
+        if (ln.store_nt < 0) ln.store_nt = 0;
         switch (cfg) {
-        case 2:
-            if constexpr (FMT == FMT_Q4_0) dispatch_z<FMT, 4, 256, 2, 1, 3, 1, 2, 2, -24>(W, x, M, bias, epi, res, out, s, ln, lnf);
-            break;
         case 3: dispatch_z<FMT, 4, 128, 4, 1, 3, 1, 0, 2, 12>(W, x, M, bias, epi, res, out, s, ln, lnf); break;
         case 16: dispatch_z<FMT, 4, 64, 4, 1, 3, 2, 3, 2, 24>(W, x, M, bias, epi, res, out, s, ln, lnf); break;
         default: dispatch_z<FMT, 2, 64, 4, 1, 3, 1, 0, 2, 24>(W, x, M, bias, epi, res, out, s, ln, lnf); break;
@@ -935,7 +913,7 @@ static int forward_cfg()
 
 bool gemm_fold_ok(const DevWeight &W, int32_t M, int32_t G)
 {
-    return G > 0 && M > 0 && M % 64 == 0 && 32 * G == (W.kx ? W.kx : W.K) && G <= fold_cap(pick_cfg(W.N, M, forward_cfg()), W.fmt);
+    return G > 0 && M > 0 && M % 64 == 0 && 32 * G == (W.kx ? W.kx : W.K) && G <= fold_cap(pick_cfg(W.N, M, forward_cfg()));
 }
 
 // CUs of the calling thread's current device, cached per ordinal (a context may

@@ -260,16 +260,14 @@ def ln_row_stats_f32(part, d):
 @pytest.mark.parametrize("fmt", [1, 2, 8])
 @pytest.mark.parametrize("epi", [0, 1])
 @pytest.mark.parametrize("N,K,M,cfg", [(1152, 384, 4096, 0), (1536, 384, 200, 3), (2304, 768, 32, 0),
-                                       (3072, 768, 64, 16), (768, 768, 1000, 4), (192, 64, 10, 0),
-                                       (2304, 768, 1000, 2), (3072, 768, 512, 2), (1152, 384, 300, 2)])
+                                       (3072, 768, 64, 16), (768, 768, 1000, 4), (192, 64, 10, 0)])
 def test_gemm_statistics_fold(lib, fmt, epi, N, K, M, cfg):
     """The statistics fold of the small-batch forward (LnFold::in_part): the GEMM
     combines the residual GEMM's per-group partials itself.  Its statistics are
     bitwise the statistics kernel's (ln_stats, the launch form) and within rounding
     of ln_row_stats restated in numpy float32, and its output is bitwise the output
     of the same GEMM given those statistics, for every fold config (3: 128-row
-    tiles up to d 384; 4, 16: 64-row tiles and 2: q4_0's 256-row tiles, partials
-    loaded after the K loop, up to d 768)."""
+    tiles up to d 384; 4, 16: 64-row tiles up to d 768)."""
     rng = np.random.default_rng(fmt * 5 + epi + N + M)
     W = rng.standard_normal((N, K)).astype(np.float32) * 0.05
     wb, deq = weight_rows(fmt, W)
@@ -289,9 +287,6 @@ def test_gemm_statistics_fold(lib, fmt, epi, N, K, M, cfg):
     stk = np.zeros((M, 2), np.float32)
     rc = lib.bertx_test_gemm_fold(fmt, N, K, wb, f32p(bias), M, z.ctypes.data, part.ctypes.data, f32p(g), f32p(be),
                                   epi, out.ctypes.data, st.ctypes.data, stk.ctypes.data, cfg)
-    if cfg == 2 and fmt != 2:
-        assert rc == -2, rc          # the 256-row fold form is q4_0's only: "no fold form"
-        return
     assert rc == 0, rc
     # bitwise the statistics kernel's combine of the same partials (the launch form)
     assert np.array_equal(st.view(np.uint32), stk.view(np.uint32))
