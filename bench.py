@@ -59,7 +59,27 @@ def parse():
     p.add_argument("--inproc-arch", default="bge-large-en-v1.5")
     p.add_argument("--inproc-ftype", default="q4_1")
     p.add_argument("--inproc-batch", type=int, default=256)
+    p.add_argument("--no-encode", action="store_true", help="skip the text-in bert_encode_batch leg")
+    p.add_argument("--dry-step", action="store_true",
+                   help="CPU stub in place of the forward (no GPU, gloo): tests the launch / timing / reporting "
+                        "skeleton, never a measurement")
     return p.parse_args()
+
+
+def launch_ranks(a):
+    """`python bench.py --gpus N` (N > 1) without a torchrun environment: start the N
+    rank processes here -- torch.distributed.run as a CHILD process, before this
+    process has imported torch or touched a GPU (never a re-exec of a process that
+    has initialised the GPU) -- and exit with its status.  Rank 0 prints the JSON
+    line to the inherited stdout."""
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.run(cmd, env=env).returncode
 
 
 def dist_env():
@@ -80,9 +100,10 @@ def algorithmic_bytes(hp, ftype, B, L):
     return w + small + emb_rows + 4 * B * L + 4 * B * d
 
 
-def timed_steps(step, steps, sync, dist=None, reduce_device="cpu"):
+def timed_steps(step, steps, sync, dist=None, reduce_device="cpu", per_rank=None):
     """The contract's timed region: barrier + sync, `steps` steps, sync + barrier;
-    returns the MAX over ranks of the elapsed seconds (every rank gets it)."""
+    returns the MAX over ranks of the elapsed seconds (every rank gets it).  With a
+    list `per_rank`, it also receives every rank's own elapsed seconds (all_gather)."""
     if dist is not None:
         dist.barrier()
     sync()
@@ -95,9 +116,16 @@ def timed_steps(step, steps, sync, dist=None, reduce_device="cpu"):
     elapsed = time.perf_counter() - t0
     if dist is not None:
         import torch
+        if per_rank is not None:
+            mine = torch.tensor([elapsed], dtype=torch.float64, device=reduce_device)
+            allv = [torch.zeros_like(mine) for _ in range(dist.get_world_size())]
+            dist.all_gather(allv, mine)
+            per_rank.extend(float(v.item()) for v in allv)
         tt = torch.tensor([elapsed], dtype=torch.float64, device=reduce_device)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
+    elif per_rank is not None:
+        per_rank.append(elapsed)
     return elapsed
 
 
@@ -354,6 +382,52 @@ def library_path(model, ids_list, steps, dist, red_dev):
     return el
 
 
+def encode_path(lib, model, ids_list, steps, dist, red_dev, ref):
+    """SURVEY §8d end-to-end: the same batch as TEXT through bert_encode_batch
+    (bert.cpp:1374-1444, the entry examples/sample_dylib.py:57-59 calls): tokenize
+    on the library's pool, sort and chunk, stage, H2D, forward, D2H into the
+    caller's rows.  Each text is the bench's ids as words of the synthetic vocab
+    ('w<i>' = id 104 + i, bertpy.synthetic_vocab), so it tokenizes to exactly those
+    512 ids.  Tokenizer threads = this job's CPU share.  Also times the tokenizer
+    stage alone (bertx_tokenize_batch, bert_encode_batch's first stage) to report
+    its share of the call."""
+    import numpy as np
+    texts = [" ".join("w%d" % (int(t) - 104) for t in ids[1:-1]).encode() for ids in ids_list]
+    toks, n = model.tokenize(texts[0])
+    if n != len(ids_list[0]) or toks != [int(x) for x in ids_list[0]]:
+        raise RuntimeError("encode texts do not tokenize to the bench ids")
+    share = len(os.sched_getaffinity(0))
+    n_thr = max(1, min(share, int(os.environ.get("OMP_NUM_THREADS", share))))
+    B, d = len(texts), model.n_embd
+    out = np.zeros((B, d), np.float32)
+    rows = (out.ctypes.data + out.strides[0] * np.arange(B, dtype=np.uintp)).astype(np.uintp)
+    rows_p = rows.ctypes.data_as(ctypes.POINTER(ctypes.POINTER(ctypes.c_float)))
+    carr = (ctypes.c_char_p * B)(*texts)
+
+    def call():
+        lib.bert_encode_batch(model.ctx, n_thr, B, B, carr, rows_p)
+    for _ in range(2):
+        call()
+    same = bool(ref is not None and np.array_equal(out, ref))
+    cos = float(np.min(np.sum(out * ref, axis=1))) if ref is not None else None
+    el = timed_steps(call, steps, lambda: None, dist, red_dev)
+    nmax = model.n_max_tokens
+    ids_buf = np.zeros((B, nmax), np.int32)
+    lens = np.zeros(B, np.int32)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        if lib.bertx_tokenize_batch(model.ctx, n_thr, B, carr, nmax, ids_buf.ctypes.data, lens.ctypes.data) != 0:
+            raise RuntimeError("bertx_tokenize_batch failed")
+    tok_s = (time.perf_counter() - t0) / steps
+    world = dist.get_world_size() if dist is not None else 1
+    return {"value": round(B * world * steps / el, 2), "unit": "sentences/s", "ms_per_step": round(el / steps * 1e3, 4),
+            "tokenizer_ms": round(tok_s * 1e3, 4), "tokenizer_share": round(tok_s / (el / steps), 4),
+            "tokenizer_threads": n_thr, "bitwise_equal_to_device_path": same, "min_cosine_vs_device_path": cos,
+            "workload": f"the same {B} sentences per GPU as text ({len(ids_list[0])} tokens each, single-token "
+                        "vocab words) through bert_encode_batch(n_batch_size = n_inputs): tokenization, staging, "
+                        "H2D, forward, D2H inside the timed region, one context per rank"}
+
+
 def run_inproc(a):
     """--inproc: ONE process drives a.gpus GPUs through the library's own multi-GPU
     path (bert_abi.cpp run_forward: sentences split over the context's GPUs by FLOP
@@ -397,13 +471,36 @@ def flop_per_sentence(hp, L):
     return nl * (2 * L * (4 * d * d + 2 * d * f) + 4 * L * L * d)
 
 
+class DryForward:
+    """--dry-step: a CPU stand-in for DeviceForward (no library, no GPU) so the
+    multi-rank launch, timing and reporting skeleton runs under gloo on a CPU host."""
+
+    def __init__(self, B, d=768):
+        self.B, self.d, self.model = B, d, None
+
+    def step(self):
+        time.sleep(0.002)
+
+    def sync(self):
+        pass
+
+    def check(self):
+        return None
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ and not a.inproc:
+        # a plain `python bench.py --gpus N`: start the N ranks (before any GPU call here)
+        sys.exit(launch_ranks(a))
     rank, world, local = dist_env()
     if a.inproc:
         assert world == 1, "--inproc runs in one process"
         run_inproc(a)
         return
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE {world}: every GPU is one rank "
+                         "(run `python bench.py --gpus N`, or torchrun with --nproc-per-node N)")
     os.environ["BERT_DEVICES"] = str(local)
     import numpy as np
     import torch
@@ -412,56 +509,70 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        backend = "gloo" if a.dry_step else ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend)
-    else:
+    elif not a.dry_step:
         torch.cuda.set_device(local)
 
     hp = bertpy.ARCHS[a.arch]
-    path = os.path.join(a.model_dir, f"{a.arch}-{a.ftype}-seed{a.seed}.bin")
-    if rank == 0:
-        path = ensure_model(bertpy, a.model_dir, a.arch, a.ftype, a.seed)
-    if dist is not None:
-        dist.barrier()
-
-    lib = bertpy.load_lib()
-    dev = torch.device("cuda", local)
-    # a non-default stream: the library captures the forward into a HIP graph
-    # (capture is impossible on the legacy null stream)
-    stream = torch.cuda.Stream(dev)
-    torch.cuda.set_stream(stream)
     B, L = a.batch, a.seq
     ids_list = bertpy.synthetic_ids(B, L, hp["n_vocab"], seed=7 + rank)
-    fwd = DeviceForward(lib, bertpy, torch, path, ids_list, dev, stream)
-    model, step = fwd.model, fwd.step
-    d = model.n_embd
+    path = os.path.join(a.model_dir, f"{a.arch}-{a.ftype}-seed{a.seed}.bin")
+    if a.dry_step:
+        fwd = DryForward(B, hp["n_embd"])
+        dev, stream, lib, model = None, None, None, None
+        sync = fwd.sync
+    else:
+        if rank == 0:
+            path = ensure_model(bertpy, a.model_dir, a.arch, a.ftype, a.seed)
+        if dist is not None:
+            dist.barrier()
+        lib = bertpy.load_lib()
+        dev = torch.device("cuda", local)
+        # a non-default stream: the library captures the forward into a HIP graph
+        # (capture is impossible on the legacy null stream)
+        stream = torch.cuda.Stream(dev)
+        torch.cuda.set_stream(stream)
+        fwd = DeviceForward(lib, bertpy, torch, path, ids_list, dev, stream)
+        model = fwd.model
+        sync = lambda: torch.cuda.synchronize(dev)
+    step = fwd.step
 
     for _ in range(a.warmup):
         step()
-    torch.cuda.synchronize(dev)
+    sync()
     e = fwd.check()
 
     red_dev = dev if (dist is not None and dist.get_backend() == "nccl") else "cpu"
     # timed region (the metric): graph replay of the forward, no per-kernel events
-    lib.bertx_set_profiling(model.ctx, 0)
-    elapsed = timed_steps(step, a.steps, lambda: torch.cuda.synchronize(dev), dist, red_dev)
+    if lib is not None:
+        lib.bertx_set_profiling(model.ctx, 0)
+    rank_elapsed = []
+    elapsed = timed_steps(step, a.steps, sync, dist, red_dev, per_rank=rank_elapsed)
     # roofline pass: the same K steps again, launched eagerly with a HIP event
     # pair around every kernel on the launch stream (per-kernel averages)
     stats = []
-    if not a.no_profile:
+    profiled = lib is not None and not a.no_profile
+    if profiled:
         lib.bertx_set_profiling(model.ctx, 1)
         lib.bertx_reset_stats(model.ctx)
-        prof_elapsed = timed_steps(step, a.steps, lambda: torch.cuda.synchronize(dev), dist, red_dev)
+        prof_elapsed = timed_steps(step, a.steps, sync, dist, red_dev)
         lib.bertx_set_profiling(model.ctx, 0)
         stats = model.kernel_stats()
 
     ms_per_step = elapsed / a.steps * 1e3
     value = B * world * a.steps / elapsed
     lib_el = None
-    if not a.no_library:
+    if lib is not None and not a.no_library:
         lib_el = library_path(model, ids_list, a.steps, dist, red_dev)
+    enc = None
+    if lib is not None and not a.no_encode:
+        try:
+            enc = encode_path(lib, model, ids_list, a.steps, dist, red_dev, e)
+        except Exception as ex:   # a report, never the metric
+            enc = {"error": str(ex)}
 
     roofline = None
     kernels = {}
@@ -473,7 +584,7 @@ def main():
     for s in stats:
         if s["launches"]:
             kernels[s["name"]]["share"] = round(s["ms"] / tot_ms, 4)
-    if stats and not a.no_profile:
+    if stats and profiled:
         dom = max(stats, key=lambda s: s["ms"])
         if dom["launches"]:
             avg_s = dom["ms"] / dom["launches"] * 1e-3
@@ -491,7 +602,7 @@ def main():
     # this run's HBM counters for the headline workload (rank 0 of a single-process
     # run: two rocprofv3 --pmc passes over build/bin/bert_probe on the same model)
     pm = None
-    if rank == 0 and world == 1 and not a.no_pmc:
+    if rank == 0 and world == 1 and not a.no_pmc and lib is not None:
         try:
             pm = pmc_live(path, B, L, device=local)
         except Exception as ex:   # a report, never the metric
@@ -517,7 +628,9 @@ def main():
         "metric": "sentences/sec + HBM GB/s, bge-base-en-v1.5 q4_0 seq512 batch64, 1/2/4/8 GPU",
         "value": round(value, 2), "unit": "sentences/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "f16", "data": "synthetic (random-init weights, seeded token ids)",
+        "dtype": "f16",
+        "data": "dry-step CPU stub (no forward; launch/timing skeleton only)" if a.dry_step
+                else "synthetic (random-init weights, seeded token ids)",
         "config": {"workload": f"{a.arch} {a.ftype} seq_len {L}, {B} sentences per GPU: bertx_forward_device on "
                                f"HBM-resident token ids (the bert_forward_batch graph without its H2D/D2H)",
                    "batch_per_gpu": B, "global_batch": B * world, "seq_len": L, "weights": a.ftype,
@@ -528,9 +641,12 @@ def main():
         "compulsory_gbps": round(alg_bytes / (ms_per_step * 1e-3) / 1e9, 2),
         "timing": "value: K graph-replayed forwards (no events); roofline/kernels: a second pass of K eager "
                   "forwards with HIP events around every kernel"
-                  + ("" if a.no_profile else f" ({prof_elapsed / a.steps * 1e3:.3f} ms/step)"),
+                  + (f" ({prof_elapsed / a.steps * 1e3:.3f} ms/step)" if profiled else ""),
         "roofline": roofline,
         "kernels": kernels,
+        # every rank's own rate over the same timed region (value uses the max time)
+        "per_rank": [{"rank": r, "sentences_per_s": round(B * a.steps / t, 2), "ms_per_step": round(t / a.steps * 1e3, 4)}
+                     for r, t in enumerate(rank_elapsed)],
     }
     # measured HBM traffic of the step: this run's PMC bytes of one forward over the
     # graph-replayed step time
@@ -549,7 +665,9 @@ def main():
                                            "arrays into host float rows (the ctypes client's path: staging, "
                                            "H2D, forward, D2H inside the timed region), one context per rank"}
 
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if enc is not None:
+        res["encode_path"] = enc
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and lib is not None:
         try:
             import oracle_lib
             # the GPU box gives one GPU's job a 16-CPU share (OMP_NUM_THREADS=16 there;
@@ -573,7 +691,7 @@ def main():
         except Exception as ex:  # the baseline is a report, never the product
             res["cpu_baseline"] = {"value": None, "error": str(ex)}
 
-    if rank == 0 and world == 1 and not a.no_probes:
+    if rank == 0 and world == 1 and not a.no_probes and lib is not None:
         try:
             res["probes"] = probes(lib, bertpy, torch, a, dev, stream, path)
         except Exception as ex:   # a probe is a report, never the metric

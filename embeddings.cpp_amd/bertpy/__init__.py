@@ -367,7 +367,7 @@ def outlier_channels(d, seed=1234):
     return np.sort(np.random.default_rng(seed + 1).choice(d, 3, replace=False))
 
 
-def synthetic_tensors(hp, seed=1234, profile="survey"):
+def synthetic_tensors(hp, seed=1234, profile="survey", qk_std=None):
     """Random weights, numpy default_rng(seed).
 
     profile "survey" (the bench's weights): matrices and biases
@@ -388,7 +388,10 @@ def synthetic_tensors(hp, seed=1234, profile="survey"):
     profile "sharp_mean": "sharp" plus a constant +16 on every channel of the
     O-proj and FFN-down biases, so every pre-LN residual row carries a mean of
     ~16 against a spread of a few units (the regime where the LN fold's
-    z = f16(y * gamma) rounds with |y| rather than |y - mean|)."""
+    z = f16(y * gamma) rounds with |y| rather than |y - mean|).
+
+    qk_std (sharp profiles): overrides the Q/K matrices' spread (the q8-activation
+    envelope sweep, scripts/q8_envelope.py)."""
     rng = np.random.default_rng(seed)
     d, f = hp["n_embd"], hp["n_intermediate"]
     shapes = {"word": (hp["n_vocab"], d), "pos": (hp["n_max_tokens"], d), "type": (2, d), "dd": (d, d),
@@ -399,7 +402,7 @@ def synthetic_tensors(hp, seed=1234, profile="survey"):
     # Q/K spread: 24 layers of peaked attention amplify the reference's own q8
     # activation rounding (bge-large at 0.05: oracle vs the same oracle with f32
     # activations 0.88 cosine; at 0.02: >= 0.99966, the 3-token sentence worst)
-    qk_std = np.float32(0.05 if hp["n_layer"] <= 12 else 0.02)
+    qk_std = np.float32(qk_std if qk_std is not None else 0.05 if hp["n_layer"] <= 12 else 0.02)
     out = {}
     for name, role in tensor_names(hp["n_layer"]):
         s = np.float32(0.02)
@@ -422,12 +425,12 @@ def synthetic_tensors(hp, seed=1234, profile="survey"):
     return out
 
 
-def synthetic_model(path, arch, ftype="q4_0", seed=1234, lib=None, profile="survey"):
+def synthetic_model(path, arch, ftype="q4_0", seed=1234, lib=None, profile="survey", qk_std=None):
     """Write a random-init model of `arch` in `ftype`.  Quantized files follow
     run_conversions.sh:5-8: f32 -> f16 file -> quantize from the f16 values."""
     hp = ARCHS[arch] if isinstance(arch, str) else arch
     vocab = synthetic_vocab(hp["n_vocab"])
-    tensors = synthetic_tensors(hp, seed, profile)
+    tensors = synthetic_tensors(hp, seed, profile, qk_std)
     if ftype in ("f32", "f16"):
         write_model(path, hp, vocab, tensors, FTYPE[ftype])
         return path

@@ -63,7 +63,9 @@ private:
                 f = std::move(q_.front());
                 q_.pop_front();
             }
-            f();
+            // nothing may leave the worker thread (std::terminate); run_forward's
+            // tasks catch their own failures, this is the last line
+            try { f(); } catch (...) { std::fprintf(stderr, "libbert: replica worker task failed\n"); }
         }
     }
     std::mutex mu_;
@@ -216,26 +218,53 @@ int run_forward(bert_ctx *ctx, const int32_t *const *toks, const int32_t *lens, 
         ctx->inflight[(size_t)dv] -= load[(size_t)dv];
         if (ctx->inflight[(size_t)dv] < 0.5) ctx->inflight[(size_t)dv] = 0.0;   // idle again (no float drift)
     };
+    // One share, exception-safe: a failure (bad_alloc staging the chunk, a throwing
+    // forward) becomes that share's rc, and `finish` always runs, so the replica
+    // counts as idle again and no task outlives this frame with an exception.
+    auto run_share = [&](int dv) noexcept {
+        try {
+            work(dv);
+        } catch (const std::exception &ex) {
+            std::fprintf(stderr, "libbert: replica %d share failed: %s\n", dv, ex.what());
+            rcs[(size_t)dv] = -1;
+        } catch (...) {
+            std::fprintf(stderr, "libbert: replica %d share failed\n", dv);
+            rcs[(size_t)dv] = -1;
+        }
+        finish(dv);
+    };
     std::vector<int> used;
     for (int dv : chosen) if (!assign[(size_t)dv].empty()) used.push_back(dv);
     if (used.size() <= 1 || ctx->workers.size() != (size_t)nd) {
-        for (int dv : used) { work(dv); finish(dv); }
+        for (int dv : used) run_share(dv);
     } else {
-        // the other shares on their replicas' persistent workers, the first on this thread
+        // the other shares on their replicas' persistent workers, the first on this
+        // thread; `left` counts only the tasks actually posted (a post that throws
+        // runs its share here), and this frame outlives every posted task
         std::mutex mu;
         std::condition_variable cv;
-        size_t left = used.size() - 1;
+        size_t left = 0;
         for (size_t i = 1; i < used.size(); ++i) {
             const int dv = used[i];
-            ctx->workers[(size_t)dv]->post([&, dv] {
-                work(dv);
-                finish(dv);
+            {
                 std::lock_guard<std::mutex> lk(mu);
-                if (--left == 0) cv.notify_one();
-            });
+                ++left;
+            }
+            try {
+                ctx->workers[(size_t)dv]->post([&, dv] {
+                    run_share(dv);
+                    std::lock_guard<std::mutex> lk(mu);
+                    if (--left == 0) cv.notify_one();
+                });
+            } catch (...) {
+                {
+                    std::lock_guard<std::mutex> lk(mu);
+                    --left;
+                }
+                run_share(dv);
+            }
         }
-        work(used[0]);
-        finish(used[0]);
+        run_share(used[0]);
         std::unique_lock<std::mutex> lk(mu);
         cv.wait(lk, [&] { return left == 0; });
     }

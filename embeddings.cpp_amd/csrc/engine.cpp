@@ -641,7 +641,7 @@ int Device::launch_all(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, in
         r1.res_stats = st_; r1.res_g = gz; r1.res_b = bz;
         r1.g_next = L.ln1_w; r1.part = part_; r1.part_stride = (int32_t)rows_;
         begin(K_GEMM_O, s, ev);
-        launch_gemm(L.o, att_, M, L.b_o, EPI_BIAS_RES, z_, z_, s, r1);
+        if (launch_gemm(L.o, att_, M, L.b_o, EPI_BIAS_RES, z_, z_, s, r1) != 0) return -1;   // refused: z_ would be stale
         end(K_GEMM_O, s, ev, 2.0 * t * d * d);
         chk("gemm_o", l, z_, (size_t)T * d, 1);
 
@@ -666,7 +666,7 @@ int Device::launch_all(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, in
         r2.res_stats = st_; r2.res_g = gz; r2.res_b = bz;
         r2.g_next = L.ln2_w; r2.part = part_; r2.part_stride = (int32_t)rows_;
         begin(K_GEMM_FFN_DOWN, s, ev);
-        launch_gemm(L.down, ffn_, M, L.b_down, EPI_BIAS_RES, z_, z_, s, r2);
+        if (launch_gemm(L.down, ffn_, M, L.b_down, EPI_BIAS_RES, z_, z_, s, r2) != 0) return -1;
         end(K_GEMM_FFN_DOWN, s, ev, 2.0 * t * d * f);
         chk("gemm_down", l, z_, (size_t)T * d, 1);
 
@@ -1030,12 +1030,14 @@ extern "C" int32_t bertx_bench_gemm(int32_t fmt, int32_t N, int32_t K, int32_t M
         ln.c1 = (const float *)B.up(hg.data(), (size_t)N * 4, 0);
     }
     if (B.bad) return -1;
+    int lrc = 0;
     auto launch = [&]() {
         g_gemm_cfg = cfg;
-        launch_gemm(W, (const uint16_t *)dx, Mp, dbias, epi, dout, dout, nullptr, ln);
+        lrc |= launch_gemm(W, (const uint16_t *)dx, Mp, dbias, epi, dout, dout, nullptr, ln);
         g_gemm_cfg = 0;
     };
     for (int i = 0; i < 3; ++i) launch();
+    if (lrc != 0) return -1;
     hipEvent_t a, b;
     HIP_RC(hipEventCreate(&a));
     HIP_RC(hipEventCreate(&b));

@@ -325,11 +325,6 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
         xvo[i] = (uint32_t)(r * KX + (((lane & 7) ^ ((r >> 1) & 7)) * 8)) * 2u;
     }
     auto issue_x_piece = [&](int ks, int stage, int i) {
-#if defined(GEMM_ABLATE) && (GEMM_ABLATE & 1)
-        // diagnostic build only: no X staging (wrong results; the K loop's cost
-        // without its LDS-DMA pieces)
-        if (ks > 0) return;
-#endif
         char *dst = PRIV ? smem + (wave * NS + stage) * XBW : smem + stage * XB + ((8 * XG * wave) << 7);
         const int kc = ks < KSX ? ks : ks - KSX;   // the X column block of K-step ks
         __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_void_t *)(dst + (i << 10)), 16, xvo[i & 1],
@@ -644,14 +639,7 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
         constexpr int NP = NJ / 2, PW = NP < 4 ? NP : 4;
         uint4 rr[PW][2];
         auto ldres = [&](int jp) {
-#if defined(GEMM_ABLATE) && (GEMM_ABLATE & 4)
-            // diagnostic build only: every residual row read from the tile's first
-            // 32 rows (L2-hot; wrong results): the epilogue without its load latency
-            // (profiles/r04_gemm_residual_lds_ab.log)
-            const int tok = m0 + 16 * (g & 1) + fr;
-#else
             const int tok = m0 + mt + 16 * (2 * jp + (g & 1)) + fr;
-#endif
 #pragma unroll
             for (int a = 0; a < 2; ++a)
                 rr[jp % PW][a] = *(const uint4 *)((const h16 *)res + (size_t)tok * N + cb + 16 * a);

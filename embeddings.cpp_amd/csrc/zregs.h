@@ -56,16 +56,6 @@ struct ZRegsQ4 {
     __device__ void pin_all() { zpin(q); zpin(d); if (FMT == FMT_Q4_1) zpin(m); }
     __device__ h16x8 frag(int u) const
     {
-#if defined(GEMM_ABLATE) && (GEMM_ABLATE & 2)
-        // diagnostic build only: no dequantization (wrong results; the K loop's
-        // cost without its VALU expansion)
-        {
-            const uint32_t w = u == 0 ? q.x : u == 1 ? q.y : u == 2 ? q.z : q.w;
-            const uint32_t dd = d.x;
-            uint4 r = {w, dd, w ^ dd, w + dd};
-            return __builtin_bit_cast(h16x8, r);
-        }
-#endif
         const uint32_t w = u == 0 ? q.x : u == 1 ? q.y : u == 2 ? q.z : q.w;
         const h16 dh = zh(d, u);
         const h16x2 d2 = {dh, dh};

@@ -67,7 +67,7 @@ public:
     {
         std::lock_guard<std::mutex> g(mu_);
         clients_ += delta;
-        cv_in_.notify_one();
+        cv_in_.notify_all();   // several batchers wait on cv_in_: wake the one whose window closed
     }
 
     // queues r and blocks until r->emb holds its embedding
@@ -75,7 +75,7 @@ public:
     {
         std::unique_lock<std::mutex> lk(mu_);
         queue_.push_back(r);
-        cv_in_.notify_one();
+        cv_in_.notify_all();
         cv_out_.wait(lk, [&] { return r->done; });
     }
 

@@ -1,0 +1,40 @@
+#!/bin/bash
+# Round-5 GPU session.  STEPS selects (test bench prof envelope stamps share tok),
+# TAG names gpurun_out/<TAG>.  Every GPU step has its own limit; a fault, abort or
+# time limit ends the script.
+set -o pipefail
+TAG=${TAG:-r05a}
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp PARITY_LOG=$OUT/parity.jsonl
+STEPS=${STEPS:-"test bench prof"}
+TESTS=${TESTS:-tests}
+has() { [[ " $STEPS " == *" $1 "* ]]; }
+step() { local lim=$1; shift; timeout -k 10 $lim "$@"; }
+if has test; then
+  step 900 python -u -m pytest ${PYX:--x} -q -rf --timeout 300 --timeout-method thread -m gpu $TESTS > $OUT/gputest.log 2>&1
+  rc=$?
+  tail -3 $OUT/gputest.log
+  [ $rc -eq 0 ] || [ $rc -eq 1 ] || { tail -40 $OUT/gputest.log; exit 1; }
+fi
+if has bench; then
+  step 400 python -u bench.py ${BENCH_ARGS:-} > $OUT/bench.log 2>&1 || { tail -20 $OUT/bench.log; exit 1; }
+  tail -c 600 $OUT/bench.log
+fi
+if has prof; then
+  ( cd /tmp && step 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --no-pmc --no-library --no-encode --no-probes --steps 10 > $GRAFT_REPO_ROOT/$OUT/prof.log 2>&1 ) || { tail -20 $OUT/prof.log; exit 1; }
+fi
+if has envelope; then
+  step 600 python -u scripts/q8_envelope.py --out $OUT/q8_envelope.jsonl > $OUT/envelope.log 2>&1 || { tail -20 $OUT/envelope.log; exit 1; }
+fi
+if has stamps; then
+  # the shipped 256 x 128 form (cfg 2) at C3 for the four GEMMs: N K epi
+  for shp in "2304 768 0" "768 768 2" "3072 768 1" "768 3072 2"; do
+    STAMPS_LIB=build/stamps/libbert.so step 120 python -u scripts/gemm_stamps.py $shp 2 >> $OUT/stamps.log 2>&1 || { tail -20 $OUT/stamps.log; exit 1; }
+  done
+fi
+if has share; then
+  step 300 python -u scripts/share_curve.py --out $OUT/share_curve.jsonl > $OUT/share.log 2>&1 || { tail -20 $OUT/share.log; exit 1; }
+fi
+if has tok; then step 300 python -u scripts/host_throughput.py tok --texts 4000 > $OUT/tok.log 2>&1 || exit 1; fi
+echo session-ok

@@ -6,8 +6,9 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT="$(pwd)"
 OUT="$ROOT/gpurun_out"
 TAG="${1:-pmc}"
-ARGS="${BENCH_ARGS:---steps 2 --warmup 1 --no-cpu-baseline --no-profile --no-probes --no-library}"
-# (no --no-pmc: bench.py sees the profiler preload itself and skips its nested passes)
+ARGS="${BENCH_ARGS:---steps 2 --warmup 1 --no-cpu-baseline --no-profile --no-probes --no-library --no-pmc}"
+# (--no-pmc: no nested rocprofv3 passes from the profiled process; bench.py's
+# under_profiler() check is the second safeguard, not the only one)
 # PMC_SCRIPT: profile that python script (repo-relative) instead of bench.py
 TARGET="$ROOT/${PMC_SCRIPT:-bench.py}"
 [ -n "${PMC_SCRIPT:-}" ] && ARGS="${PMC_SCRIPT_ARGS:-}"

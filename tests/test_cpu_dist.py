@@ -106,3 +106,34 @@ def test_pmc_passes_skip_under_a_profiler(monkeypatch):
     monkeypatch.setattr(subprocess, "run", refuse)
     r = bench.pmc_live("/nonexistent.bin", 1, 32)
     assert "skipped" in r and "bytes_per_forward" not in r
+
+
+def test_bench_gpus_2_starts_two_ranks():
+    """`python bench.py --gpus 2` with no torchrun environment starts its two rank
+    processes itself -- here with the --dry-step CPU stub on
+    gloo: exactly one JSON line, n_gpus 2, one per-rank entry per rank, and the
+    value is the whole job's rate (both ranks' sentences over the max time)."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-step", "--steps", "4",
+                        "--warmup", "1"], cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr.decode()[-2000:]
+    lines = [x for x in r.stdout.decode().splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout.decode()
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["config"]["global_batch"] == 128
+    assert [p["rank"] for p in res["per_rank"]] == [0, 1]
+    t_max = max(p["ms_per_step"] for p in res["per_rank"])
+    assert abs(res["ms_per_step"] - t_max) < 1e-3
+    assert abs(res["value"] - 128 * 1e3 / res["ms_per_step"]) / res["value"] < 1e-3
+
+
+def test_bench_refuses_world_mismatch():
+    """A rank whose WORLD_SIZE disagrees with --gpus stops before any work."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-step"], cwd="/tmp",
+                       env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=120)
+    assert r.returncode != 0 and b"WORLD_SIZE 1" in r.stderr

@@ -257,7 +257,7 @@ def ln_row_stats_f32(part, d):
     return np.stack([mean, r], axis=1).astype(f)
 
 
-@pytest.mark.parametrize("fmt", [1, 2, 8])
+@pytest.mark.parametrize("fmt", [1, 2, 3, 8])
 @pytest.mark.parametrize("epi", [0, 1])
 @pytest.mark.parametrize("N,K,M,cfg", [(1152, 384, 4096, 0), (1536, 384, 200, 3), (2304, 768, 32, 0),
                                        (3072, 768, 64, 16), (768, 768, 1000, 4), (192, 64, 10, 0)])

@@ -34,7 +34,7 @@ def _recv_exact(sock, n):
 
 
 @pytest.mark.parametrize("devices", ["0", "0,0,0,0"])
-def test_microbatch_server_concurrent_clients(quant_models, devices):
+def test_microbatch_server_concurrent_clients(quant_models, devices, monkeypatch):
     """One replica (one batcher), and four replicas on the one GPU (BERT_DEVICES=0,0,0,0:
     four batchers, each micro-batch routed whole to the least-loaded replica)."""
     if not os.path.exists(EXE):
@@ -85,7 +85,7 @@ def test_microbatch_server_concurrent_clients(quant_models, devices):
         proc.kill()
         proc.wait(timeout=30)
 
-    os.environ["BERT_DEVICES"] = "0"
+    monkeypatch.setenv("BERT_DEVICES", "0")
     m = bertpy.BertModel(path)
     o = oracle_lib.Oracle(path)
     for k in range(n_cli):
