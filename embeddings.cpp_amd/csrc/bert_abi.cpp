@@ -96,13 +96,16 @@ namespace {
 constexpr int64_t kChunkTokens = 1 << 17;   // tokens per device forward (workspace bound)
 constexpr int kChunkSeqs = 4096;            // sentences per device forward (pool / output staging bound)
 // A call is split only over replicas that are idle (no routed work in flight), and
-// only while each share keeps at least kMinShareTokens: below that a forward is
-// launch- and latency-bound (C2's 4,096 tokens run in 0.37 ms, B = 1 in 0.56 ms),
-// so a smaller share buys little latency and costs its replica a whole forward.  A
-// call that finds no idle replica goes whole to the least-loaded one, so concurrent
+// only while each share keeps at least kMinShareTokens.  Measured per-share latency
+// on one replica (scripts/share_curve.py, profiles/r05_share_curve.jsonl: bge-base
+// q4_0, 128-token sentences through bert_forward_batch): the cost per token is 4.7x
+// the large-batch asymptote at 128 tokens, 1.8x at 4,096, 1.26x at 8,192 and 1.07x
+// at 16,384 -- below 8,192 tokens a forward is launch- and latency-bound, so a
+// smaller share buys little latency and costs its replica a whole forward.  A call
+// that finds no idle replica goes whole to the least-loaded one, so concurrent
 // callers (the server's batchers) land on different replicas instead of all
 // splitting over all of them in lockstep.
-constexpr int64_t kMinShareTokens = 4096;
+constexpr int64_t kMinShareTokens = 8192;
 
 std::vector<int> parse_device_list(int n_visible)
 {

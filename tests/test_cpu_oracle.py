@@ -216,3 +216,28 @@ def test_oracle_encode_batch(oracle):
     for t, e in zip(texts, out):
         single = orc.forward_batch([orc.tokenize(t)])[0]
         assert float(np.dot(single, e)) > 1 - 1e-5
+
+
+def test_activation_f32_switch(oracle, quant_models):
+    """The diagnostic switch (oracle_set_activation_f32): quantized
+    weights times f32 activations instead of the reference's q8 re-quantized ones.
+    It changes only the quantized-weight matmuls (f16 / f32 files bitwise
+    unchanged), moves a tiny q4_0 model by a little (the q8 rounding), brings it
+    closer to the f32-weight forward of the same model, and is restored after the
+    call."""
+    z = np.load(f"{GOLDEN}/tiny64/forward_f32.npz")
+    seqs = np.split(z["ids"], np.cumsum(z["lens"])[:-1])[:6]
+    ref = oracle.Oracle(quant_models[("tiny64", "f32")]).forward_batch(seqs)
+    for fmt in ("f16", "f32"):
+        o = oracle.Oracle(quant_models[("tiny64", fmt)])
+        assert np.array_equal(o.forward_batch(seqs), o.forward_batch(seqs, activations="f32"))
+    o = oracle.Oracle(quant_models[("tiny64", "q8_0")])
+    q8 = o.forward_batch(seqs)
+    f32 = o.forward_batch(seqs, activations="f32")
+    assert oracle.lib().oracle_get_activation_f32() == 0
+    assert not np.array_equal(q8, f32)
+    c_q8 = np.sum(q8 * ref, axis=1)
+    c_f32 = np.sum(f32 * ref, axis=1)
+    assert np.all(np.sum(q8 * f32, axis=1) > 1 - 1e-3)
+    assert np.mean(1 - c_f32) <= np.mean(1 - c_q8)
+    assert np.array_equal(o.forward_batch(seqs), q8)
