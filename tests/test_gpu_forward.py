@@ -90,6 +90,40 @@ def test_batch_composition_invariance(quant_models):
     assert np.array_equal(rev[::-1], full)
 
 
+def test_stats_fold_forward_bitwise(quant_models, tmp_path):
+    """The small-batch statistics fold (engine.cpp: QKV / FFN-up combine their input's
+    LN statistics from the residual GEMM's partials; 2 n_layer - 1 fewer ln_stats
+    launches) gives the bits of the launch form end to end.  The switch
+    is a process-wide static (BERT_STATS_FOLD), so each form runs in its own
+    process on the same ids, for every quantized format and both tile families the
+    fold runs on (64-row tiles at a few tokens, 128-row tiles at a few hundred)."""
+    import subprocess
+    import sys
+    ids = ragged_ids(690, [5, 17, 32, 60], seed=4)
+    big = ragged_ids(690, [300, 290, 310, 512], seed=5)
+    allx = ids + big
+    np.savez(tmp_path / "ids.npz", flat=np.concatenate(allx).astype(np.int32), lens=[len(x) for x in allx])
+    code = (
+        "import sys, numpy as np\n"
+        f"sys.path.insert(0, {os.path.join(os.path.dirname(bertpy.__file__), '..')!r})\n"
+        "import bertpy\n"
+        "m = bertpy.BertModel(sys.argv[1])\n"
+        "z = np.load(sys.argv[2])\n"
+        "ids = np.split(z['flat'], np.cumsum(z['lens'])[:-1])\n"
+        "np.save(sys.argv[3], np.concatenate([m.forward_batch(ids[:4]), m.forward_batch(ids[4:])]))\n")
+    for fmt in ("q4_0", "q4_1", "q8_0", "f16"):
+        outs = []
+        for fold in ("0", "1"):
+            out = tmp_path / f"{fmt}_{fold}.npy"
+            env = dict(os.environ, BERT_STATS_FOLD=fold, BERT_DEVICES="0")
+            r = subprocess.run([sys.executable, "-c", code, quant_models[("tiny64", fmt)], str(tmp_path / "ids.npz"),
+                                str(out)], env=env, capture_output=True, timeout=120)
+            assert r.returncode == 0, r.stderr.decode()[-2000:]
+            outs.append(np.load(out))
+        assert np.all(np.isfinite(outs[0]))
+        assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32)), fmt
+
+
 def test_fake_batch_and_forward(quant_models):
     """bert_forward_fake_batch and bert_forward against the oracle's restatements
     (oracle_forward_fake_batch: bert.cpp:1151-1363; bert_forward = a batch of one,
