@@ -92,7 +92,6 @@ struct ZSet {
 #pragma unroll
         for (int f = 0; f < FA; ++f) r[f].pin_all();
     }
-    __device__ __forceinline__ void pin_h() { r[0].pin_h(); }   // half record (HALF waves)
 };
 
 // One K-step's MFMAs: B fragments (s, j) -> item i = s NJ + j, read PF items
@@ -114,30 +113,22 @@ __device__ __forceinline__ void zmma_pre(h16x8 (&bq)[PF + 1], uint32_t b0, uint3
 // ALLDQ: all four A fragments of a 32-feature group dequantized up front (short
 // K-steps, where the mid-step dequantization sat on the critical path), else
 // the second k-slice's at item NJ (fewer live registers).
-// HALF: the wave computes one 16-feature half of the group (the half record in
-// slots 0 / 1: frag(0) k-slice 0, frag(1) k-slice 1) into acc[0]: one MFMA per item.
-template <int NJ, int FA, int PF, bool PRE, bool ALLDQ, bool HALF, class R, class H, int... I>
+template <int NJ, int FA, int PF, bool PRE, bool ALLDQ, class R, class H, int... I>
 __device__ __forceinline__ void zmma_items(const R &cur, uint32_t b0, uint32_t b1, f32x4 (&acc)[2 * FA][NJ],
                                            const H &hook, h16x8 (&bq)[PF + 1], std::integer_sequence<int, I...> seq)
 {
     constexpr int NI = 2 * NJ;
-    constexpr int NA = HALF ? 1 : 2 * FA;        // MFMAs per B fragment
     auto rd = [&](auto ic) {
         constexpr int i = decltype(ic)::value;
         if constexpr (i < NI) bq[i % (PF + 1)] = zds_read<(i % NJ) << 11>(i < NJ ? b0 : b1);
     };
     if constexpr (!PRE) zmma_pre<NJ, PF>(bq, b0, b1, seq);
     h16x8 af[2 * FA], af2[ALLDQ ? 2 * FA : 1];
-    if constexpr (HALF) {
-        af[0] = cur.r[0].frag(0);
-        if constexpr (ALLDQ) af2[0] = cur.r[0].frag(1);
-    } else {
 #pragma unroll
-        for (int f = 0; f < FA; ++f) { af[2 * f] = cur.r[f].frag(0); af[2 * f + 1] = cur.r[f].frag(2); }
-        if constexpr (ALLDQ) {
+    for (int f = 0; f < FA; ++f) { af[2 * f] = cur.r[f].frag(0); af[2 * f + 1] = cur.r[f].frag(2); }
+    if constexpr (ALLDQ) {
 #pragma unroll
-            for (int f = 0; f < FA; ++f) { af2[2 * f] = cur.r[f].frag(1); af2[2 * f + 1] = cur.r[f].frag(3); }
-        }
+        for (int f = 0; f < FA; ++f) { af2[2 * f] = cur.r[f].frag(1); af2[2 * f + 1] = cur.r[f].frag(3); }
     }
     auto item = [&](auto ic) {
         constexpr int i = decltype(ic)::value;
@@ -148,9 +139,7 @@ __device__ __forceinline__ void zmma_items(const R &cur, uint32_t b0, uint32_t b
         if constexpr (i == NJ) {
             if constexpr (ALLDQ) {
 #pragma unroll
-                for (int u = 0; u < NA; ++u) af[u] = af2[u];
-            } else if constexpr (HALF) {
-                af[0] = cur.r[0].frag(1);
+                for (int u = 0; u < 2 * FA; ++u) af[u] = af2[u];
             } else {
 #pragma unroll
                 for (int f = 0; f < FA; ++f) { af[2 * f] = cur.r[f].frag(1); af[2 * f + 1] = cur.r[f].frag(3); }
@@ -158,7 +147,7 @@ __device__ __forceinline__ void zmma_items(const R &cur, uint32_t b0, uint32_t b
         }
         const h16x8 bf = bq[i % (PF + 1)];
 #pragma unroll
-        for (int u = 0; u < NA; ++u)
+        for (int u = 0; u < 2 * FA; ++u)
             acc[u][i % NJ] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[u], bf, acc[u][i % NJ], 0, 0, 0);
     };
     (item(std::integral_constant<int, I>{}), ...);
@@ -268,22 +257,15 @@ static_assert(z_waits<4, 4, 2, 4>().front == 3 * 6 && z_waits<4, 4, 2, 4>().back
 // The tile body: workgroup b of a grid of nTiles tiles (nN column tiles),
 // staging X in `smem` (NS * BM * 128 B of LDS) and the epilogue operands
 // behind it (zepi_lds).
-template <int FMT, int EPI, bool LNF, int NW, int BM, int NS, int FA, int WR, int NT, int XI, int GF, bool HALF>
+template <int FMT, int EPI, bool LNF, int NW, int BM, int NS, int FA, int WR, int NT, int XI, int GF>
 __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b, DevWeight W,
                                            const h16 *__restrict__ X, const float *__restrict__ bias,
                                            const void *__restrict__ res, void *__restrict__ out, int nN, int nTiles,
                                            const LnFold &ln)
 {
-    // NT waves along the tokens (each BM / NT of them), NW / NT along the features.
-    // HALF (small batches): wave pairs (2p, 2p + 1) share 32-feature group p of the
-    // tile, each computing one 16-feature half over all BM tokens: half the
-    // dequantization per wave of the 32-feature form and twice the waves per tile;
-    // after the K loop the odd wave hands its accumulators to the even one through
-    // LDS, which runs the 32-feature epilogue unchanged -- every output comes from
-    // the same MFMA chain as in every other config, so the same bits.
+    // NT waves along the tokens (each BM / NT of them), NW / NT along the features
     static_assert(NW % NT == 0 && (BM / NT) % 32 == 0, "wave grid");
-    static_assert(!HALF || (FA == 1 && NT == 1 && NW % 2 == 0 && XI == 0), "half waves");
-    constexpr int NF = HALF ? NW / 2 : NW / NT;   // 32-feature groups across the tile
+    constexpr int NF = NW / NT;
     constexpr int BN = 32 * NF * FA;
     constexpr int NJ = BM / NT / 16;            // 16-token B fragments per k-slice (this wave's tokens)
     constexpr int PF = FA == 1 ? (NJ <= 4 ? 2 * NJ - 1 : 4) : 3;   // B-fragment read-ahead (items of 2 FA MFMAs)
@@ -299,7 +281,7 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     constexpr int XBW = (BM / NT) * ZK * 2;     // bytes per wave-private stage
     constexpr int RING = PRIV ? NW * NS * XBW : NS * XB;
     constexpr int XG = PRIV ? XBW / 1024 : XB / (64 * NW * 16);   // LDS-DMA instructions per wave per stage
-    constexpr int LQ = HALF ? ZRegs<FMT>::LOADS_H : ZRegs<FMT>::LOADS * FA;
+    constexpr int LQ = ZRegs<FMT>::LOADS * FA;
     constexpr int QB = ZRegs<FMT>::QB;
     constexpr int P = LQ + XG;                  // vector-memory ops issued per K-step per wave
     static_assert(NS >= 2 && NS <= 4 && XG >= 2 && XG % 2 == 0, "X ring");
@@ -318,10 +300,8 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     const int K = W.K, N = W.N, KS = K / ZK;
     const int KX = W.kx ? W.kx : K, KSX = KX / ZK;   // X columns (f32 hi/lo weights: K = 2 KX)
     const int fr = lane & 15, g = lane >> 4;
-    const int wf = HALF ? wave >> 1 : wave % NF;   // this wave's 32-feature group in the tile
-    const int ah = HALF ? wave & 1 : 0;            // HALF: the 16-feature half it computes
-    const int mt = HALF ? 0 : (BM / NT) * (wave / NF);   // this wave's first token row in the tile
-    const int nw = n0 + 32 * FA * wf;           // this wave's first feature (its group's)
+    const int mt = (BM / NT) * (wave / NF);     // this wave's first token row in the tile
+    const int nw = n0 + 32 * FA * (wave % NF);  // this wave's first feature
     const int grp = min(nw, N - 32) >> 5;       // its first 32-feature weight group (clamped past N)
     // the wave's further groups (clamped past N; wave-uniform byte / element offsets)
     int gq[FA], gd[FA];
@@ -359,15 +339,10 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     const uint16_t *wmn = FMT == FMT_Q4_1 ? W.m + ((size_t)grp * 16 + fr) * 4 : nullptr;
     const size_t qstep = (size_t)N * 2 * QB, sstep = (size_t)N * 2;
     auto wload = [&](ZSet<FMT, FA> &w, int ks) {
-        if constexpr (HALF) {
-            w.r[0].load_h(wq + ks * qstep + gq[0], wd + ks * sstep + gd[0],
-                          FMT == FMT_Q4_1 ? wmn + ks * sstep + gd[0] : nullptr, ah);
-        } else {
 #pragma unroll
-            for (int f = 0; f < FA; ++f)
-                w.r[f].load(wq + ks * qstep + gq[f], wd + ks * sstep + gd[f],
-                            FMT == FMT_Q4_1 ? wmn + ks * sstep + gd[f] : nullptr);
-        }
+        for (int f = 0; f < FA; ++f)
+            w.r[f].load(wq + ks * qstep + gq[f], wd + ks * sstep + gd[f],
+                        FMT == FMT_Q4_1 ? wmn + ks * sstep + gd[f] : nullptr);
     };
 
     // epilogue operands -> LDS (wave 0; retired by the prologue's vmcnt wait,
@@ -499,7 +474,7 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
             }
             wait_vmcnt<ZW.front>();
             cur.pin_all();
-            zmma_items<NJ, FA, PF, true, true, false>(cur, b0, b1, acc, hook, bq, std::make_integer_sequence<int, 2 * NJ>{});
+            zmma_items<NJ, FA, PF, true, true>(cur, b0, b1, acc, hook, bq, std::make_integer_sequence<int, 2 * NJ>{});
             wait_vmcnt<ZW.back>();
         } else {
             if constexpr (XMODE) {
@@ -529,12 +504,11 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
                 zw_front += __builtin_amdgcn_s_memtime() - za;
 #endif
             }
-            if constexpr (HALF) cur.pin_h();
-            else cur.pin_all();
+            cur.pin_all();
             const uint32_t xs = lds_u32(smem + st * XB + rbase);
             h16x8 bq[PF + 1];
-            zmma_items<NJ, FA, PF, false, false, HALF>(cur, xs + ((g ^ sw) << 4), xs + (((4 + g) ^ sw) << 4), acc, hook,
-                                                       bq, std::make_integer_sequence<int, 2 * NJ>{});
+            zmma_items<NJ, FA, PF, false, false>(cur, xs + ((g ^ sw) << 4), xs + (((4 + g) ^ sw) << 4), acc, hook, bq,
+                                                 std::make_integer_sequence<int, 2 * NJ>{});
 #ifdef GEMM_STAMPS
             const unsigned long long zb = __builtin_amdgcn_s_memtime();
 #endif
@@ -615,20 +589,6 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
             if (n0 == 0 && ln.st_out) ln.st_out[m0 + tid] = rs;
         }
         lds_barrier();
-    }
-    if constexpr (HALF) {
-        // the odd wave of each pair hands its 16-feature half (acc[0]) to the even
-        // wave (its acc[1]) through LDS behind the tail scratch slot; the even wave
-        // runs the 32-feature epilogue, the odd one is done with the tile
-        char *const xch = smem + RING + zepi_lds<EPI, LNF, BN, BM, GF>() + 256 + (wf * NJ * 64 + lane) * 16;
-        if (ah) {
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) *(f32x4 *)(xch + j * 1024) = acc[0][j];
-        }
-        lds_barrier();
-        if (ah) return;
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[1][j] = *(const f32x4 *)(xch + j * 1024);
     }
     ZSTAMP(2, __builtin_amdgcn_s_memtime());
 #ifdef GEMM_STAMPS
@@ -792,22 +752,20 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     }
 }
 
-template <int FMT, int EPI, bool LNF, int NW, int BM, int NS, int FA, int WR, int NT, int XI, int OCC, int GF, bool HALF>
+template <int FMT, int EPI, bool LNF, int NW, int BM, int NS, int FA, int WR, int NT, int XI, int OCC, int GF>
 __global__ __launch_bounds__(64 * NW, OCC * NW / 4) void gemmz_kernel(DevWeight W, const h16 *__restrict__ X,
                                                                const float *__restrict__ bias,
                                                                const void *__restrict__ res, void *__restrict__ out,
                                                                int nN, int nTiles, LnFold ln)
 {
-    constexpr int BNK = 32 * (HALF ? NW / 2 : NW / NT) * FA;
-    __shared__ __attribute__((aligned(16))) char smem[(XI >= 3 ? NW / NT : 1) * NS * BM * ZK * 2 + zepi_lds<EPI, LNF, BNK, BM, GF>() +
-                                                      256 +   // + the tail steps' scratch slot (ztail_dma)
-                                                      (HALF ? (NW / 2) * (BM / 16) * 1024 : 0)];   // + HALF's hand-off
+    __shared__ __attribute__((aligned(16))) char smem[(XI >= 3 ? NW / NT : 1) * NS * BM * ZK * 2 + zepi_lds<EPI, LNF, 32 * (NW / NT) * FA, BM, GF>() +
+                                                      256];   // + the tail steps' scratch slot (ztail_dma)
     // a grid smaller than nTiles walks the tiles b, b + grid, ... (persistent;
     // the host only launches it so when every wave of every tile has features,
     // so no wave leaves the body early and the barrier between tiles is reached
     // by all)
     for (int b = blockIdx.x; b < nTiles; b += gridDim.x) {
-        gemmz_body<FMT, EPI, LNF, NW, BM, NS, FA, WR, NT, XI, GF, HALF>(smem, b, W, X, bias, res, out, nN, nTiles, ln);
+        gemmz_body<FMT, EPI, LNF, NW, BM, NS, FA, WR, NT, XI, GF>(smem, b, W, X, bias, res, out, nN, nTiles, ln);
         ZSTAMP(3, __builtin_amdgcn_s_memtime());
         if (b + (int)gridDim.x < nTiles) lds_barrier();   // LDS (X ring, epilogue operands) reused
     }
@@ -815,12 +773,11 @@ __global__ __launch_bounds__(64 * NW, OCC * NW / 4) void gemmz_kernel(DevWeight 
 
 // OCC: workgroups per CU the launch bounds ask registers for (2: two co-resident
 // tiles; 3: three, at most 168 VGPRs per wave)
-template <int FMT, int NW, int BM, int NS, int FA = 1, int WR = 3, int NT = 1, int XI = 0, int OCC = 2, int GF = 0,
-          bool HALF = false>
+template <int FMT, int NW, int BM, int NS, int FA = 1, int WR = 3, int NT = 1, int XI = 0, int OCC = 2, int GF = 0>
 void dispatch_z(const DevWeight &W, const h16 *x, int M, const float *bias, int epi, const void *res, void *out,
                 hipStream_t s, const LnFold &ln, bool lnf)
 {
-    constexpr int BN = 32 * (HALF ? NW / 2 : NW / NT) * FA;
+    constexpr int BN = 32 * (NW / NT) * FA;
     const int nN = (W.N + BN - 1) / BN, nTiles = (M / BM) * nN;
     // Persistent when a launch is at most two rounds of two workgroups per CU
     // (the N = d GEMMs at C3: 768 tiles = 1.5 rounds): 2 workgroups per CU walk
@@ -836,17 +793,17 @@ void dispatch_z(const DevWeight &W, const h16 *x, int M, const float *bias, int 
     auto go = [&](auto kern) { kern<<<grid, 64 * NW, 0, s>>>(W, x, bias, res, out, nN, nTiles, ln); };
     if constexpr (GF > 0) {
         // statistics fold: the input-LN forms only (launch_fmt checked epi / lnf)
-        if (epi == EPI_BIAS_F16) go(gemmz_kernel<FMT, EPI_BIAS_F16, true, NW, BM, NS, FA, WR, NT, XI, OCC, GF, HALF>);
-        else go(gemmz_kernel<FMT, EPI_BIAS_GELU_F16, true, NW, BM, NS, FA, WR, NT, XI, OCC, GF, HALF>);
+        if (epi == EPI_BIAS_F16) go(gemmz_kernel<FMT, EPI_BIAS_F16, true, NW, BM, NS, FA, WR, NT, XI, OCC, GF>);
+        else go(gemmz_kernel<FMT, EPI_BIAS_GELU_F16, true, NW, BM, NS, FA, WR, NT, XI, OCC, GF>);
     } else if (epi == EPI_BIAS_F16) {
-        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_F16, true, NW, BM, NS, FA, WR, NT, XI, OCC, 0, HALF>);
-        else go(gemmz_kernel<FMT, EPI_BIAS_F16, false, NW, BM, NS, FA, WR, NT, XI, OCC, 0, HALF>);
+        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_F16, true, NW, BM, NS, FA, WR, NT, XI, OCC, 0>);
+        else go(gemmz_kernel<FMT, EPI_BIAS_F16, false, NW, BM, NS, FA, WR, NT, XI, OCC, 0>);
     } else if (epi == EPI_BIAS_GELU_F16) {
-        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_GELU_F16, true, NW, BM, NS, FA, WR, NT, XI, OCC, 0, HALF>);
-        else go(gemmz_kernel<FMT, EPI_BIAS_GELU_F16, false, NW, BM, NS, FA, WR, NT, XI, OCC, 0, HALF>);
+        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_GELU_F16, true, NW, BM, NS, FA, WR, NT, XI, OCC, 0>);
+        else go(gemmz_kernel<FMT, EPI_BIAS_GELU_F16, false, NW, BM, NS, FA, WR, NT, XI, OCC, 0>);
     } else {
-        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_RES, true, NW, BM, NS, FA, WR, NT, XI, OCC, 0, HALF>);
-        else go(gemmz_kernel<FMT, EPI_BIAS_RES, false, NW, BM, NS, FA, WR, NT, XI, OCC, 0, HALF>);
+        if (lnf) go(gemmz_kernel<FMT, EPI_BIAS_RES, true, NW, BM, NS, FA, WR, NT, XI, OCC, 0>);
+        else go(gemmz_kernel<FMT, EPI_BIAS_RES, false, NW, BM, NS, FA, WR, NT, XI, OCC, 0>);
     }
 }
 
@@ -858,7 +815,6 @@ void dispatch_z(const DevWeight &W, const h16 *x, int M, const float *bias, int 
 //   4   2 waves 64 x 64                                small batches, >= half the CUs
 //   16  4 waves 64 x 64, 2 along the tokens, wave-private X rings
 //                                                      small batches, < half the CUs
-//   17  4 waves 64 x 64, 16 features per wave (HALF)   small batches (A/B: BERT_GEMM_SMALL)
 // A config whose row tile does not divide M falls back to the next smaller tile.
 // The tile config a launch of N features over M rows runs (cfg 0: the heuristic),
 // after the fallbacks for tiles that do not divide M.
@@ -876,20 +832,19 @@ int pick_cfg(int N, int M, int cfg)
         // else on 2 (C2's O-proj and FFN-down: the 4-wave forms 6-15 % slower
         // there).  Same bits either way.
         const long n64 = (long)(M / 64) * ((N + 63) / 64);
-        static const int small_env = [] { const char *e = std::getenv("BERT_GEMM_SMALL"); return e ? std::atoi(e) : 0; }();
-        const int small = small_env ? small_env : 2 * n64 < cus ? 16 : 4;
+        const int small = 2 * n64 < cus ? 16 : 4;
         cfg = (M % 256 == 0 && (M / 256) * n128 >= 2 * cus) ? 2 : (M % 128 == 0 && (M / 128) * n128 >= cus) ? 3 : small;
     }
     if ((cfg == 2 || cfg == 11) && M % 256) cfg = 3;
     if (cfg == 3 && M % 128) cfg = 4;
-    if (cfg != 2 && cfg != 11 && cfg != 3 && cfg != 16 && cfg != 17) cfg = 4;
+    if (cfg != 2 && cfg != 11 && cfg != 3 && cfg != 16) cfg = 4;
     return cfg;
 }
 
 // Statistics-fold capacity (LnFold::in_part) of a config: the partial groups its
 // LDS holds (cfg 3 keeps two workgroups per CU with 12: d <= 384; the 64-row
 // forms with 24: d <= 768); 0 = no fold form (the 256-row large-batch tiles).
-constexpr int fold_cap(int cfg) { return cfg == 3 ? 12 : (cfg == 4 || cfg == 16 || cfg == 17) ? 24 : 0; }
+constexpr int fold_cap(int cfg) { return cfg == 3 ? 12 : (cfg == 4 || cfg == 16) ? 24 : 0; }
 
 template <int FMT>
 int launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, int32_t epi, const void *res,
@@ -905,7 +860,6 @@ int launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, i
         switch (cfg) {
         case 3: dispatch_z<FMT, 4, 128, 4, 1, 3, 1, 0, 2, 12>(W, x, M, bias, epi, res, out, s, ln, lnf); break;
         case 16: dispatch_z<FMT, 4, 64, 4, 1, 3, 2, 3, 2, 24>(W, x, M, bias, epi, res, out, s, ln, lnf); break;
-        case 17: dispatch_z<FMT, 4, 64, 4, 1, 3, 1, 0, 2, 24, true>(W, x, M, bias, epi, res, out, s, ln, lnf); break;
         default: dispatch_z<FMT, 2, 64, 4, 1, 3, 1, 0, 2, 24>(W, x, M, bias, epi, res, out, s, ln, lnf); break;
         }
         return cfg;
@@ -927,7 +881,6 @@ int launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, i
     case 11: dispatch_z<FMT, 4, 256, 2>(W, x, M, bias, epi, res, out, s, ln, lnf); break;
     case 3: dispatch_z<FMT, 4, 128, 4>(W, x, M, bias, epi, res, out, s, ln, lnf); break;
     case 16: dispatch_z<FMT, 4, 64, 4, 1, 3, 2, 3>(W, x, M, bias, epi, res, out, s, ln, lnf); break;
-    case 17: dispatch_z<FMT, 4, 64, 4, 1, 3, 1, 0, 2, 0, true>(W, x, M, bias, epi, res, out, s, ln, lnf); break;
     default: dispatch_z<FMT, 2, 64, 4>(W, x, M, bias, epi, res, out, s, ln, lnf); break;
     }
     return cfg;

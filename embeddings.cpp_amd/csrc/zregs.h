@@ -30,8 +30,6 @@ __device__ __forceinline__ void zpin(uint2 &q)
     q = __builtin_bit_cast(uint2, v);
 }
 
-__device__ __forceinline__ void zpin(uint32_t &q) { asm volatile("" : "+v"(q)); }
-
 __device__ __forceinline__ h16 zh(uint2 v, int u)   // f16 number u (0..3) of an 8-byte word pair
 {
     const uint32_t w = u < 2 ? v.x : v.y;
@@ -48,7 +46,6 @@ struct ZRegsQ4 {
     uint4 q;           // word u: 8 nibbles, element i at bit 4*(i/2) + 16*(i%2)
     uint2 d, m;        // f16 scale (and min) of fragment u
     static constexpr int LOADS = FMT == FMT_Q4_1 ? 3 : 2;
-    static constexpr int LOADS_H = LOADS;
     static constexpr int QB = 16;
     __device__ void load(const uint8_t *pq, const uint16_t *pd, const uint16_t *pm)
     {
@@ -56,18 +53,7 @@ struct ZRegsQ4 {
         d = zload8(pd);
         if (FMT == FMT_Q4_1) m = zload8(pm);
     }
-    // Half record (16-feature waves, gemm.hip HALF): fragments u = 2 ah, 2 ah + 1 of
-    // the lane record (features +16 ah, k-slices 0 and 1) into slots 0 and 1, so
-    // frag(0) / frag(1) are that half's two k-slices.
-    __device__ void load_h(const uint8_t *pq, const uint16_t *pd, const uint16_t *pm, int ah)
-    {
-        const uint2 h = zload8(pq + 8 * ah);
-        q.x = h.x; q.y = h.y;
-        d.x = *(const uint32_t *)(pd + 2 * ah);
-        if (FMT == FMT_Q4_1) m.x = *(const uint32_t *)(pm + 2 * ah);
-    }
     __device__ void pin_all() { zpin(q); zpin(d); if (FMT == FMT_Q4_1) zpin(m); }
-    __device__ void pin_h() { zpin(q.x); zpin(q.y); zpin(d.x); if (FMT == FMT_Q4_1) zpin(m.x); }
     __device__ h16x8 frag(int u) const
     {
         const uint32_t w = u == 0 ? q.x : u == 1 ? q.y : u == 2 ? q.z : q.w;
@@ -105,7 +91,6 @@ struct ZRegs<FMT_Q8_0> {
     uint4 q0, q1;      // 8 bytes per fragment u at 8u: (q ^ 0x80), order e0 e2 e1 e3 per 4-group
     uint2 d;
     static constexpr int LOADS = 3;
-    static constexpr int LOADS_H = 2;
     static constexpr int QB = 32;
     __device__ void load(const uint8_t *pq, const uint16_t *pd, const uint16_t *)
     {
@@ -113,13 +98,7 @@ struct ZRegs<FMT_Q8_0> {
         q1 = zload16(pq + 16);
         d = zload8(pd);
     }
-    __device__ void load_h(const uint8_t *pq, const uint16_t *pd, const uint16_t *, int ah)
-    {
-        q0 = zload16(pq + 16 * ah);
-        d.x = *(const uint32_t *)(pd + 2 * ah);
-    }
     __device__ void pin_all() { zpin(q0); zpin(q1); zpin(d); }
-    __device__ void pin_h() { zpin(q0); zpin(d.x); }
     __device__ h16x8 frag(int u) const
     {
         const uint32_t w0 = u == 0 ? q0.x : u == 1 ? q0.z : u == 2 ? q1.x : q1.z;
@@ -142,24 +121,17 @@ template <>
 struct ZRegs<FMT_F16> {
     uint4 q[4];        // fragment u: 8 f16
     static constexpr int LOADS = 4;
-    static constexpr int LOADS_H = 2;
     static constexpr int QB = 64;
     __device__ void load(const uint8_t *pq, const uint16_t *, const uint16_t *)
     {
 #pragma unroll
         for (int i = 0; i < 4; ++i) q[i] = zload16(pq + 16 * i);
     }
-    __device__ void load_h(const uint8_t *pq, const uint16_t *, const uint16_t *, int ah)
-    {
-        q[0] = zload16(pq + 32 * ah);
-        q[1] = zload16(pq + 32 * ah + 16);
-    }
     __device__ void pin_all()
     {
 #pragma unroll
         for (int i = 0; i < 4; ++i) zpin(q[i]);
     }
-    __device__ void pin_h() { zpin(q[0]); zpin(q[1]); }
     __device__ h16x8 frag(int u) const { return __builtin_bit_cast(h16x8, q[u]); }
 };
 

@@ -158,17 +158,16 @@ def test_f32_gemm_matches_numpy(lib, epi, N, K, M):
 
 
 @pytest.mark.parametrize("fmt", sorted(FMTS))
-@pytest.mark.parametrize("cfg", [2, 3, 4, 11, 16, 17])
+@pytest.mark.parametrize("cfg", [2, 3, 4, 11, 16])
 def test_gemm_every_k_remainder(lib, cfg, fmt):
     """Every K-loop length from 1 to 7 K-steps (K = 64 .. 448), every epilogue, for each
     shipped tile config -- 2: 256x128 (X ring NS 2, the pieces among the MFMAs), 3: 128x128,
     4: 64x64, 11: 256x128 with the X pieces in one burst in front of the MFMAs, 16: 64x64 on 4
-    waves (2 along the tokens) with wave-private X rings (no barrier in the K loop), 17: 64x64 on
-    4 waves of 16 features (the HALF form: half records, accumulator hand-off) -- so every
+    waves (2 along the tokens) with wave-private X rings (no barrier in the K loop) -- so every
     remainder of the unrolled K loop (triples) and every prologue clamp runs against numpy, and
     the kernel that ran is the one asked for (bertx_test_gemm_ran).  The waits these paths rely
     on are derived, not hand-counted (gemm.hip z_waits)."""
-    N = {2: 256, 3: 256, 4: 128, 11: 256, 16: 128, 17: 128}[cfg]
+    N = {2: 256, 3: 256, 4: 128, 11: 256, 16: 128}[cfg]
     M = 256
     for ks in range(1, 8):
         K = 64 * ks
@@ -201,8 +200,7 @@ def f32p(a):
 @pytest.mark.parametrize("fmt", [0, 1, 2, 3, 8])
 @pytest.mark.parametrize("epi", [0, 1])
 @pytest.mark.parametrize("N,K,M,cfg", [(2304, 768, 512, 0), (384, 1536, 300, 3), (1024, 1024, 768, 2),
-                                       (1536, 384, 96, 4), (3072, 768, 256, 16), (768, 768, 512, 11),
-                                       (2304, 768, 64, 17)])
+                                       (1536, 384, 96, 4), (3072, 768, 256, 16), (768, 768, 512, 11)])
 def test_gemm_input_ln_fold(lib, fmt, epi, N, K, M, cfg):
     """Projection of a LayerNorm'd stream as the forward runs it (kernels.h LN fold):
     the GEMM reads z = f16(y * gamma) and the row statistics of y, and returns
@@ -262,8 +260,7 @@ def ln_row_stats_f32(part, d):
 @pytest.mark.parametrize("fmt", [1, 2, 3, 8])
 @pytest.mark.parametrize("epi", [0, 1])
 @pytest.mark.parametrize("N,K,M,cfg", [(1152, 384, 4096, 0), (1536, 384, 200, 3), (2304, 768, 32, 0),
-                                       (3072, 768, 64, 16), (768, 768, 1000, 4), (192, 64, 10, 0),
-                                       (3072, 768, 64, 17), (1536, 384, 300, 17)])
+                                       (3072, 768, 64, 16), (768, 768, 1000, 4), (192, 64, 10, 0)])
 def test_gemm_statistics_fold(lib, fmt, epi, N, K, M, cfg):
     """The statistics fold of the small-batch forward (LnFold::in_part): the GEMM
     combines the residual GEMM's per-group partials itself.  Its statistics are
@@ -306,8 +303,7 @@ def test_gemm_statistics_fold(lib, fmt, epi, N, K, M, cfg):
 @pytest.mark.parametrize("fmt", [1, 2, 3, 8])
 @pytest.mark.parametrize("N,K,M,cfg", [(768, 768, 512, 0), (384, 1536, 256, 3), (1024, 1024, 384, 2),
                                        (768, 3072, 256, 0), (384, 1536, 130, 4), (768, 3072, 384, 11),
-                                       (768, 3072, 64, 16), (384, 1536, 130, 16), (768, 3072, 64, 17),
-                                       (384, 1536, 130, 17)])
+                                       (768, 3072, 64, 16), (384, 1536, 130, 16)])
 def test_residual_gemm_ln_statistics(lib, fmt, N, K, M, cfg):
     """Residual projection as the forward runs it: res = f16(y * gamma) with y's
     statistics (the residual is LN(y)), y' = LN(y) + x W^T + b comes back as
@@ -392,14 +388,13 @@ def test_attention_matches_numpy(lib, variant, dh):
 
 
 @pytest.mark.parametrize("fmt", [1, 2, 3, 8])
-@pytest.mark.parametrize("cfg", [2, 3, 11, 16, 17])
+@pytest.mark.parametrize("cfg", [2, 3, 11, 16])
 def test_small_tiles_bitwise_equal_to_64x64(lib, fmt, cfg):
     """Tile shape and wave layout change who computes an output, not how: every (token,
     feature) is the same k-ordered MFMA chain and the same epilogue arithmetic, so every
     shipped config gives the 64x64 tile's bits (the forward's batch-composition invariance
     rests on it), including the residual form's LN statistics: the 256- and 128-row tiles,
-    the interleaved- and burst-X forms (2, 11), the wave-private rings on 4 waves (16) and the
-    16-feature waves whose odd wave hands its accumulators to the even one (17)."""
+    the interleaved- and burst-X forms (2, 11) and the wave-private rings on 4 waves (16)."""
     N, K, M = 768, 1536, 256
     rng = np.random.default_rng(fmt + cfg)
     W = rng.standard_normal((N, K)).astype(np.float32) * 0.05
