@@ -712,289 +712,6 @@ __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restr
 
 
 
-// ---------------------------------------------------------------------------
-// attention_lds5: attention_lds3 in 32-key units instead of 64-key blocks, so
-// only one 16-register score tile is live.  The 16 freed
-// VGPRs hold the next unit's four K fragments, read from asm right after the
-// unit's exp / row-sum (behind the rare rescale path, which still needs this
-// unit's fragments) and retired by the wait in front of the next unit's QK: the
-// QK MFMAs no longer wait on an LDS read each (lds3 at 128 VGPRs reads every K
-// fragment right in front of its MFMA and waits for it).  The offset c is the
-// f16 row max of the first 32 keys; the rescale check is per unit (every P stays
-// <= 2^ATT_SUMX).  Same persistence, regions, B1 / S barriers and stores as lds3.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void attention_lds5_kernel(const h16 *__restrict__ qkv,
-                                                              const int32_t *__restrict__ cu, int d, int nh,
-                                                              int n_items, float sl2, h16 *__restrict__ out)
-{
-    constexpr int DH = 64, RB = DH * 2, LMAX = ATT_LDS_MAX, RH = LMAX / 2, NU = LMAX / 32;
-    static_assert(RH == 256, "a region is 32 pieces: two per wave");
-    __shared__ __attribute__((aligned(16))) char smem[2 * LMAX * RB];
-    char *Kl = smem;
-    const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int hi = lane >> 5, lq = lane & 31;
-    const int ld = 3 * d;
-
-    struct Item { int start, len, h; };
-    auto item = [&](int i) {
-        const int b = i / nh;
-        Item r;
-        r.h = i - b * nh;
-        r.start = cu[b];
-        r.len = cu[b + 1] - r.start;
-        return r;
-    };
-    auto issue = [&](const Item &it, int r) {             // as lds3
-        const int lane = lane_id_opaque();
-        const int nrows = (it.len + 63) & ~63;
-        const h16 *kbase = qkv + (size_t)it.start * ld + d + it.h * DH;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int i = 32 * r + w + 16 * j;
-            if (8 * i < nrows) {
-                const int row = 8 * i + (lane >> 3), pc = lane & 7;
-                const size_t so = (size_t)min(row, it.len - 1) * ld;
-                glds16_hidden(kbase + so + (pc ^ ((row >> 1) & 7)) * 8, Kl + i * 1024);
-                glds16_hidden(kbase + d + so + (pc ^ (((row >> 1) & 1) << 2)) * 8, Kl + LMAX * RB + i * 1024);
-            }
-        }
-    };
-    h16x8 qf[DH / 16];
-    auto load_q = [&](const Item &it) {
-        if (it.len <= 0) return;
-        const int lane = lane_id_opaque(), hi = lane >> 5, lq = lane & 31;
-        const h16 *qrow = qkv + (size_t)(it.start + min(32 * w + lq, it.len - 1)) * ld + it.h * DH;
-#pragma unroll
-        for (int s = 0; s < DH / 16; ++s) qf[s] = *(const h16x8 *)(qrow + 16 * s + 8 * hi);
-    };
-
-    int koff[DH / 16];
-#pragma unroll
-    for (int st = 0; st < DH / 16; ++st) koff[st] = lds_u32(Kl) + lq * RB + (((2 * st + hi) ^ ((lq >> 1) & 7)) << 4);
-    const int gi = lane & 15, gq = gi >> 2, gp = gi & 3, gg = lane >> 4;
-    const int vsw = ((gq >> 1) & 1) << 2;
-    int voff[DH / 32];
-#pragma unroll
-    for (int t = 0; t < DH / 32; ++t) {
-        const int ch = 4 * t + 2 * (gg & 1) + (gp >> 1);
-        voff[t] = (4 * (gg >> 1) + gq) * RB + ((ch ^ vsw) << 4) + 8 * (gp & 1);
-    }
-    const h16 one = (h16)1.0f, zero = (h16)0.0f;
-    const h16x8 abias = {hi ? zero : one, zero, zero, zero, zero, zero, zero, zero};
-    h16x8 bbias = {zero, zero, zero, zero, zero, zero, zero, zero};
-
-    f32x16 o[DH / 32];
-    float c = 0.f, l = 0.f;
-    f32x16 s;
-    h16x8 kf[DH / 16];                                    // K fragments of the unit about to run
-    int len = 0;
-
-    // the four K fragments of unit u (keys 32 u .. 32 u + 31) into kf, from asm
-    // (hipcc would sink plain loads next to their MFMAs).  Every kread is
-    // followed, in the same straight-line code, by kf_wait (tied to kf), so no
-    // register holding an LDS read in flight crosses a branch or join where hipcc
-    // could copy it (round 3's fault class).  Placed in front of
-    // the unit's P.V, the reads overlap the P.V reads' latency (LDS reads retire
-    // in order), and the wait behind P.V finds them landed.
-    auto kread = [&](int u) {
-#pragma unroll
-        for (int st = 0; st < DH / 16; ++st)
-            asm volatile("ds_read_b128 %0, %1" : "=v"(kf[st]) : "v"(koff[st] + u * 32 * RB));
-    };
-    auto kf_wait = [&]() {
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(kf[0]), "+v"(kf[1]), "+v"(kf[2]), "+v"(kf[3]));
-    };
-    auto qk = [&](int kb, bool bias) {                    // s = S (- c) of keys kb .. kb + 31, from kf
-        if (bias) {
-            s = __builtin_amdgcn_mfma_f32_32x32x16_f16(abias, bbias, f32x16{}, 0, 0, 0);
-        } else {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) s[r] = 0.f;
-        }
-#pragma unroll
-        for (int st = 0; st < DH / 16; ++st) s = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[st], qf[st], s, 0, 0, 0);
-        if (kb + 32 > len) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int key = kb + (r & 3) + 8 * (r >> 2) + 4 * hi;
-                if (key >= len) s[r] = -INFINITY;
-            }
-        }
-    };
-    auto row_max = [&]() {
-        float mx = s[0];
-#pragma unroll
-        for (int r = 1; r < 16; ++r) mx = fmaxf(mx, s[r]);
-        return halves_max(mx);
-    };
-    auto shift_by = [&](float sh) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) s[r] -= sh;
-    };
-    auto expsum = [&]() {
-        float rs = 0.f;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const float p = __builtin_amdgcn_exp2f(s[r]);
-            s[r] = p;
-            rs += p;
-        }
-        return rs;
-    };
-    auto pv = [&](int kb) {
-        int vbo[DH / 32];
-#pragma unroll
-        for (int t = 0; t < DH / 32; ++t) {
-            vbo[t] = voff[t] + kb * RB + LMAX * RB;
-            asm volatile("" : "+v"(vbo[t]));
-        }
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-            h16x8 bp;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) bp[j] = (h16)s[8 * s2 + j];
-#pragma unroll
-            for (int t = 0; t < DH / 32; ++t) {
-                const char *va = smem + vbo[t] + 16 * s2 * RB;
-                const h16x4 lo = lds_read_tr16(va);
-                const h16x4 up = lds_read_tr16(va + 8 * RB);
-                const h16x8 a = {lo[0], lo[1], lo[2], lo[3], up[0], up[1], up[2], up[3]};
-                o[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bp, o[t], 0, 0, 0);
-            }
-        }
-    };
-
-    int cur_i = blockIdx.x;
-    if (cur_i >= n_items) return;                         // workgroup-uniform
-    Item cur = item(cur_i);
-    load_q(cur);
-    issue(cur, 0);
-    wait_all_vm();
-    __syncthreads();
-    const h16 s16 = (h16)sl2;
-    const h16x8 sc = {s16, s16, s16, s16, s16, s16, s16, s16};
-    for (;;) {
-        const int nx_i = cur_i + (int)gridDim.x;
-        const bool more = nx_i < n_items;
-        Item nx = {0, 0, 0};
-        if (more) nx = item(nx_i);
-        len = cur.len;
-        const int nunits = (len + 31) >> 5;               // units holding keys of the sentence
-        const bool active = 32 * w < len;
-#pragma unroll
-        for (int st = 0; st < DH / 16; ++st) qf[st] *= sc;
-        asm volatile("" ::"v"(qf[0]), "v"(qf[1]), "v"(qf[2]), "v"(qf[3]));
-        issue(cur, 1);
-#pragma unroll
-        for (int t = 0; t < DH / 32; ++t)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) o[t][r] = 0.f;
-        c = 0.f;
-        l = 0.f;
-        bbias[0] = zero;
-        __builtin_amdgcn_s_setprio(3);
-        if (active) {                                     // unit 0: the offset is its row max (f16-rounded)
-            kread(0);
-            kf_wait();
-            qk(0, false);
-            c = (float)(h16)row_max();
-            shift_by(c);
-            bbias[0] = hi ? zero : (h16)(-c);
-            l = expsum();
-            kread(1);
-            pv(0);
-            kf_wait();
-        }
-#pragma clang loop unroll(disable)
-        for (int u = 1; u < NU; ++u) {
-            const int kb = 32 * u;
-            if (kb == RH) {
-                wait_all_vm();                            // this item's region-B pieces
-                __syncthreads();                          // B1: region A is free
-                if (more) issue(nx, 0);
-                if (active && u < nunits) {               // region B's first unit: read after B1
-                    kread(u);
-                    kf_wait();
-                }
-            }
-            switch ((kb >> 6) & 3) {                      // progress-based priority (lds3)
-            case 0: __builtin_amdgcn_s_setprio(3); break;
-            case 1: __builtin_amdgcn_s_setprio(2); break;
-            case 2: __builtin_amdgcn_s_setprio(1); break;
-            default: __builtin_amdgcn_s_setprio(0); break;
-            }
-            if (active && u < nunits) {
-                qk(kb, true);                             // S - c (kf landed)
-                float rs = expsum();
-                if (__builtin_amdgcn_ballot_w64(rs > (float)(1 << ATT_SUMX))) {
-                    // rare: move c to the row max, rescale, redo the unit (kf still
-                    // holds this unit's fragments)
-                    qk(kb, true);
-                    const float m = row_max();
-                    const float sh = m > 0.f ? (float)(h16)(c + m) - c : 0.f;
-                    const float alpha = __builtin_amdgcn_exp2f(-sh);
-                    shift_by(sh);
-                    c += sh;
-                    bbias[0] = hi ? zero : (h16)(-c);
-                    l *= alpha;
-#pragma unroll
-                    for (int t = 0; t < DH / 32; ++t)
-#pragma unroll
-                        for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
-                    rs = expsum();
-                }
-                l += rs;
-                // the next unit's K fragments under this unit's P.V (unconditional, so
-                // the read and its wait stay in one block: past the sentence or across
-                // the region boundary the fragments are not used -- region B's first
-                // unit is read again after B1; unit 16 lies in the V image)
-                kread(u + 1);
-                pv(kb);
-                kf_wait();
-            }
-        }
-        if (more) load_q(nx);
-        auto store_rows = [&]() {                         // as lds3
-            const float inv = 1.0f / halves_sum(l);
-            const int q = 32 * w + lq;
-            uint32_t pk[DH / 8][2];
-#pragma unroll
-            for (int m = 0; m < DH / 8; ++m)
-#pragma unroll
-                for (int k = 0; k < 2; ++k) {
-                    const int t = m >> 2, g = m & 3;
-                    const h16x2 v = {(h16)(o[t][4 * g + 2 * k] * inv), (h16)(o[t][4 * g + 2 * k + 1] * inv)};
-                    pk[m][k] = __builtin_bit_cast(uint32_t, v);
-                }
-#pragma unroll
-            for (int p = 0; p < DH / 16; ++p)
-#pragma unroll
-                for (int k = 0; k < 2; ++k) {
-                    const auto r = __builtin_amdgcn_permlane32_swap(pk[2 * p][k], pk[2 * p + 1][k], false, false);
-                    pk[2 * p][k] = r[0];
-                    pk[2 * p + 1][k] = r[1];
-                }
-            const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
-                (void *)(out + (size_t)cur.start * d), (short)0, cur.len * d * 2, 0x00020000);
-            const int ob = (q * d + cur.h * DH + 8 * hi) * 2;
-#pragma unroll
-            for (int p = 0; p < DH / 16; ++p) {
-                typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
-                const u32x4v v = {pk[2 * p][0], pk[2 * p][1], pk[2 * p + 1][0], pk[2 * p + 1][1]};
-                __builtin_amdgcn_raw_buffer_store_b128(v, ors, ob + 32 * p, 0, 0);
-            }
-        };
-        if (more) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else wait_all_vm();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // no LDS read in flight into the store phase
-        __syncthreads();                                  // S: region B is free
-        if (active) store_rows();
-        if (!more) break;
-        cur = nx;
-        cur_i = nx_i;
-    }
-}
-
 thread_local int g_att_variant = 0;   // benches only (bertx_bench_attention), per calling thread
 
 void launch_attention(const uint16_t *qkv, const int32_t *cu, int32_t n_seqs, int32_t max_len, int32_t n_head,
@@ -1007,19 +724,11 @@ void launch_attention(const uint16_t *qkv, const int32_t *cu, int32_t n_seqs, in
         if (dh == 64) {
             // 0: production (attention_lds3, persistent, one workgroup per CU); 7:
             // the same kernel on at most 7 workgroups (tests: many ragged items each)
-            // 5 / 57: attention_lds5 (32-key units, K fragments read a unit ahead),
-            // also chosen by BERT_ATT=5 (A/B)
-            static const int att_env = [] { const char *e = std::getenv("BERT_ATT"); return e ? std::atoi(e) : 0; }();
-            const int var = g_att_variant ? g_att_variant : att_env;
             const int n_items = n_seqs * n_head;
-            const int cap = (var == 7 || var == 57) ? 7 : device_cu_count();
+            const int cap = g_att_variant == 7 ? 7 : device_cu_count();
             const int grid = n_items < cap ? n_items : cap;
-            if (grid > 0) {
-                if (var == 5 || var == 57)
-                    attention_lds5_kernel<<<grid, 1024, 0, s>>>((const h16 *)qkv, cu, d, n_head, n_items, sl2, (h16 *)out);
-                else
-                    attention_lds3_kernel<<<grid, 1024, 0, s>>>((const h16 *)qkv, cu, d, n_head, n_items, sl2, (h16 *)out);
-            }
+            if (grid > 0)
+                attention_lds3_kernel<<<grid, 1024, 0, s>>>((const h16 *)qkv, cu, d, n_head, n_items, sl2, (h16 *)out);
         } else {
             attention_lds_kernel<32><<<g, blk, 0, s>>>((const h16 *)qkv, cu, d, n_head, sl2, (h16 *)out);
         }
