@@ -501,6 +501,12 @@ def main():
     if world != a.gpus:
         raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE {world}: every GPU is one rank "
                          "(run `python bench.py --gpus N`, or torchrun with --nproc-per-node N)")
+    # BENCH_SHARED_DEVICE=1 (rehearsal of the N-rank path on a one-GPU box): every
+    # rank drives GPU 0 and the timing collectives go over gloo (RCCL does not run
+    # two ranks on one GPU); the per-rank rates then share that GPU
+    shared = os.environ.get("BENCH_SHARED_DEVICE", "0") == "1" and world > 1
+    if shared:
+        local = 0
     os.environ["BERT_DEVICES"] = str(local)
     import numpy as np
     import torch
@@ -509,7 +515,7 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        backend = "gloo" if a.dry_step else ("nccl" if torch.cuda.is_available() else "gloo")
+        backend = "gloo" if (a.dry_step or shared) else ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend)
@@ -648,6 +654,8 @@ def main():
         "per_rank": [{"rank": r, "sentences_per_s": round(B * a.steps / t, 2), "ms_per_step": round(t / a.steps * 1e3, 4)}
                      for r, t in enumerate(rank_elapsed)],
     }
+    if shared:
+        res["shared_device_rehearsal"] = f"BENCH_SHARED_DEVICE=1: all {world} ranks on GPU 0 (gloo timing collectives)"
     # measured HBM traffic of the step: this run's PMC bytes of one forward over the
     # graph-replayed step time
     if pm is not None:

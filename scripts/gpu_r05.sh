@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round-5 GPU session.  STEPS selects (test bench prof envelope stamps share tok),
+# Round-5 GPU session.  STEPS selects (test bench prof pmc rehearsal envelope
+# stamps share tok),
 # TAG names gpurun_out/<TAG>.  Every GPU step has its own limit; a fault, abort or
 # time limit ends the script.
 set -o pipefail
@@ -23,6 +24,17 @@ if has bench; then
 fi
 if has prof; then
   ( cd /tmp && step 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --no-pmc --no-library --no-encode --no-probes --steps 10 > $GRAFT_REPO_ROOT/$OUT/prof.log 2>&1 ) || { tail -20 $OUT/prof.log; exit 1; }
+fi
+if has pmc; then
+  # one counter group per rocprofv3 pass over a short bench (scripts/pmc.sh passes
+  # --no-pmc itself), then the per-class summary
+  step 900 bash scripts/pmc.sh ${TAG}pmc > $OUT/pmc.log 2>&1 || { tail -20 $OUT/pmc.log; exit 1; }
+  python3 scripts/pmc_classes.py "$TAG tree, C3 bench under rocprofv3 --pmc" gpurun_out/${TAG}pmc_pmc* > $OUT/pmc_summary.txt 2>&1 || true
+fi
+if has rehearsal; then
+  # the N-rank launch path on this one-GPU box: bench.py --gpus 2 starts its two
+  # ranks itself; both drive GPU 0 (BENCH_SHARED_DEVICE=1, gloo timing collectives)
+  BENCH_SHARED_DEVICE=1 step 300 python -u bench.py --gpus 2 --steps 10 --warmup 2 --no-cpu-baseline --no-probes --no-pmc --no-library --no-encode > $OUT/rehearsal.log 2>&1 || { tail -20 $OUT/rehearsal.log; exit 1; }
 fi
 if has envelope; then
   step 600 python -u scripts/q8_envelope.py --out $OUT/q8_envelope.jsonl > $OUT/envelope.log 2>&1 || { tail -20 $OUT/envelope.log; exit 1; }
