@@ -425,11 +425,14 @@ def synthetic_tensors(hp, seed=1234, profile="survey", qk_std=None):
     return out
 
 
-def synthetic_model(path, arch, ftype="q4_0", seed=1234, lib=None, profile="survey", qk_std=None):
+def synthetic_model(path, arch, ftype="q4_0", seed=1234, lib=None, profile="survey", qk_std=None, vocab=None):
     """Write a random-init model of `arch` in `ftype`.  Quantized files follow
-    run_conversions.sh:5-8: f32 -> f16 file -> quantize from the f16 values."""
+    run_conversions.sh:5-8: f32 -> f16 file -> quantize from the f16 values.
+    vocab: the token list (default synthetic_vocab; e.g. bert_like_vocab for
+    multilingual text)."""
     hp = ARCHS[arch] if isinstance(arch, str) else arch
-    vocab = synthetic_vocab(hp["n_vocab"])
+    vocab = synthetic_vocab(hp["n_vocab"]) if vocab is None else list(vocab)
+    assert len(vocab) == hp["n_vocab"]
     tensors = synthetic_tensors(hp, seed, profile, qk_std)
     if ftype in ("f32", "f16"):
         write_model(path, hp, vocab, tensors, FTYPE[ftype])

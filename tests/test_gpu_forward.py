@@ -163,6 +163,48 @@ def test_encode_batch_matches_oracle(quant_models):
         assert np.all(c >= 1 - COS_TOL), (bs, c.min())
 
 
+def test_c5_multilingual_encode_matches_oracle(tmp_path):
+    """SURVEY §8d end-to-end at C5 dims (bge-base-zh q8_0, V 21,128) on multilingual
+    text: a BERT-like WordPiece vocab with Latin-1, Greek and CJK entries
+    (bertpy.bert_like_vocab), texts of whole words, '##'-split words, accents, digits,
+    punctuation, CJK runs and characters outside the vocab, plus all-CJK texts, from
+    a few to past 512 tokens.  Through bert_encode_batch (sorted, chunked by
+    n_batch_size; a chunk holding an over-long text is refused, as bert.cpp:1408-1443
+    does) against the oracle's encode_batch: the same token ids, the same written
+    rows, every written row within the north-star cosine."""
+    hp = bertpy.ARCHS["bge-base-zh-v1.5"]
+    vocab = bertpy.bert_like_vocab(hp["n_vocab"], seed=5)
+    path = str(tmp_path / "bge-base-zh-q8_0-multilingual.bin")
+    bertpy.synthetic_model(path, "bge-base-zh-v1.5", "q8_0", seed=1234, vocab=vocab)
+    texts = []
+    for k, nw in enumerate((3, 12, 40, 90, 160, 260)):
+        texts += bertpy.bert_like_texts(vocab, 3, nw, seed=20 + k)
+    rng = np.random.default_rng(31)
+    cjk = [w for w in vocab[104:] if len(w) == 1 and ord(w) >= 0x3400]
+    for n in (7, 60, 200, 480, 560):
+        texts.append(("".join(cjk[int(i)] + ("\u3002" if j % 17 == 16 else "")
+                              for j, i in enumerate(rng.integers(0, len(cjk), n)))).encode("utf-8"))
+    m = bertpy.BertModel(path)
+    o = oracle_lib.Oracle(path)
+    for t in texts:
+        ids, n = m.tokenize(t)
+        assert ids == o.tokenize(t)[: len(ids)] and n == len(o.tokenize(t)), t[:40]
+    lens = [m.tokenize(t)[1] for t in texts]
+    assert min(lens) < 16 and max(lens) > 512 and sum(x > 300 for x in lens) >= 3, lens
+    for bs in (8, 5, len(texts)):
+        got = m.encode(texts, batch_size=bs)
+        ref, written = o.encode_batch(texts, bs, n_threads=min(16, os.cpu_count() or 1))
+        wrote = ~np.all(got == 0.0, axis=1)
+        assert np.array_equal(wrote, written), (bs, wrote, written)
+        if bs == len(texts):                                  # one unsorted batch holding a > 512 text: refused
+            assert not written.any()
+            continue
+        assert written.sum() >= len(texts) - bs              # only the chunk with the long text refused
+        c = cosines(got[written], ref[written])
+        print(f"C5 multilingual encode, batch {bs}: {int(written.sum())} rows, min cos {c.min():.7f}")
+        assert np.all(c >= 1 - COS_TOL), (bs, c.min())
+
+
 def test_bge_base_q4_0_full_size(tmp_path):
     """BASELINE config shape: bge-base q4_0, L = 512, B = 64.  Oracle parity on two
     sentences; size-independent properties on the full batch."""
