@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round-5 GPU session.  STEPS selects (test bench prof pmc rehearsal envelope
-# stamps share tok),
+# Round-5 GPU session.  STEPS selects (test bench prof pmc rehearsal b1trace
+# envelope stamps share tok),
 # TAG names gpurun_out/<TAG>.  Every GPU step has its own limit; a fault, abort or
 # time limit ends the script.
 set -o pipefail
@@ -35,6 +35,10 @@ if has rehearsal; then
   # the N-rank launch path on this one-GPU box: bench.py --gpus 2 starts its two
   # ranks itself; both drive GPU 0 (BENCH_SHARED_DEVICE=1, gloo timing collectives)
   BENCH_SHARED_DEVICE=1 step 300 python -u bench.py --gpus 2 --steps 10 --warmup 2 --no-cpu-baseline --no-probes --no-pmc --no-library --no-encode > $OUT/rehearsal.log 2>&1 || { tail -20 $OUT/rehearsal.log; exit 1; }
+fi
+if has b1trace; then
+  # GPU-side kernel durations of the B = 1, L = 32 forward (graph replay)
+  ( cd /tmp && step 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/b1prof -o b1 --output-format csv -- python3 $GRAFT_REPO_ROOT/scripts/b1_trace.py 32 200 > $GRAFT_REPO_ROOT/$OUT/b1trace.log 2>&1 ) || { tail -20 $OUT/b1trace.log; exit 1; }
 fi
 if has envelope; then
   step 600 python -u scripts/q8_envelope.py --out $OUT/q8_envelope.jsonl > $OUT/envelope.log 2>&1 || { tail -20 $OUT/envelope.log; exit 1; }
