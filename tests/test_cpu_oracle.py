@@ -14,6 +14,8 @@ Pins (DESIGN.md "Oracle"):
   * forward: tiny models converted by the reference converter
     (models/convert-to-ggml.py) with an independent torch forward (make_golden.py).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -241,3 +243,98 @@ def test_activation_f32_switch(oracle, quant_models):
     assert np.all(np.sum(q8 * f32, axis=1) > 1 - 1e-3)
     assert np.mean(1 - c_f32) <= np.mean(1 - c_q8)
     assert np.array_equal(o.forward_batch(seqs), q8)
+
+
+def _model_tensors(oracle, path):
+    """(hparams, {name: f32 array}) of a model file in the reference format
+    (bert.cpp:434-766); quantized rows dequantized by the oracle's era dequantizer."""
+    import struct
+    L = oracle.lib()
+    f = open(path, "rb").read()
+    off = 4
+    hp = struct.unpack_from("<7i", f, off)
+    off += 28
+    for _ in range(hp[0]):
+        off += 4 + struct.unpack_from("<i", f, off)[0]
+    out = {}
+    while off < len(f):
+        nd, nl, ft = struct.unpack_from("<3i", f, off)
+        off += 12
+        ne = struct.unpack_from(f"<{nd}i", f, off)
+        off += 4 * nd
+        name = f[off:off + nl].decode()
+        off += nl
+        k, rows = ne[0], int(np.prod(ne[1:])) if nd > 1 else 1
+        rb = {0: 4 * k, 1: 2 * k, 2: k // 32 * 18, 3: k // 32 * 20, 8: k // 32 * 34}[ft]
+        buf = np.frombuffer(f, np.uint8, rb * rows, off)
+        off += rb * rows
+        if ft == 0:
+            a = buf.view(np.float32).reshape(rows, k)
+        elif ft == 1:
+            a = buf.view(np.float16).astype(np.float32).reshape(rows, k)
+        else:
+            a = np.zeros((rows, k), np.float32)
+            base = buf.ctypes.data
+            for r in range(rows):
+                L.oracle_dequantize_row(ft, base + r * rb, a[r].ctypes.data, k)
+        out[name] = a if nd > 1 else a.reshape(-1)
+    return hp, out
+
+
+def _torch_forward(hp, tensors, ids_list):
+    """An independent float forward: transformers' BertModel with the era constants
+    (tanh GELU, LayerNorm eps 1e-5) on the file's (dequantized) weights, masked mean
+    pool, L2 normalise (tests/golden/make_golden.py torch_embed)."""
+    import torch
+    from transformers import BertConfig, BertModel
+    cfg = BertConfig(vocab_size=hp[0], hidden_size=hp[2], num_attention_heads=hp[4], intermediate_size=hp[3],
+                     num_hidden_layers=hp[5], max_position_embeddings=hp[1], type_vocab_size=2,
+                     hidden_act="gelu_pytorch_tanh", layer_norm_eps=1e-5)
+    model = BertModel(cfg, add_pooling_layer=False)
+    missing, unexpected = model.load_state_dict({k: torch.tensor(np.asarray(v)) for k, v in tensors.items()},
+                                                strict=False)
+    assert not unexpected and all("position_ids" in k for k in missing), (missing, unexpected)
+    model.eval()
+    Lm = max(len(x) for x in ids_list)
+    ids = torch.full((len(ids_list), Lm), 101, dtype=torch.long)
+    mask = torch.zeros((len(ids_list), Lm), dtype=torch.long)
+    for i, x in enumerate(ids_list):
+        ids[i, : len(x)] = torch.tensor(np.asarray(x, np.int64))
+        mask[i, : len(x)] = 1
+    with torch.no_grad():
+        h = model(input_ids=ids, attention_mask=mask, token_type_ids=torch.zeros_like(ids)).last_hidden_state
+        m = mask.unsqueeze(-1).float()
+        e = (h * m).sum(1) / m.sum(1)
+        e = e / e.norm(dim=-1, keepdim=True)
+    return e.numpy().astype(np.float32)
+
+
+@pytest.mark.parametrize("arch,ftype,profile", [("all-MiniLM-L6-v2", "f32", "sharp"),
+                                                 ("bge-base-en-v1.5", "q4_0", "survey")])
+def test_oracle_pinned_to_torch_at_survey_dims(oracle, tmp_path, arch, ftype, profile):
+    """The oracle's forward against an independent torch/transformers forward at the
+    SURVEY architectures (the committed goldens pin it on tiny models only): C1's
+    MiniLM-L6 f32 file on sharp weights, and C3's bge-base architecture as a q4_0 file
+    -- torch runs the file's dequantized weights (embedding tables included) and the
+    oracle runs its f32-activation switch, so both multiply the same weights by f32
+    activations and the comparison pins the oracle's q4_0 decoding, layer order, era
+    GELU / softmax tables and pooling at full depth.  Ragged lengths (padding and mask)."""
+    import bertpy
+    hp_arch = bertpy.ARCHS[arch]
+    path = str(tmp_path / f"{arch}-{ftype}.bin")
+    if ftype == "f32":
+        bertpy.write_model(path, hp_arch, bertpy.synthetic_vocab(hp_arch["n_vocab"]),
+                           bertpy.synthetic_tensors(hp_arch, 1234, profile), 0)
+    else:
+        f16 = str(tmp_path / f"{arch}-f16.bin")
+        bertpy.write_model(f16, hp_arch, bertpy.synthetic_vocab(hp_arch["n_vocab"]),
+                           bertpy.synthetic_tensors(hp_arch, 1234, profile), 1)
+        assert oracle.quantize_file(f16, path, 2) == 0
+        os.remove(f16)
+    hp, tensors = _model_tensors(oracle, path)
+    ids = bertpy.synthetic_ids(4, [32, 17, 5, 64], hp[0], seed=7)
+    ref = _torch_forward(hp, tensors, ids)
+    got = oracle.Oracle(path).forward_batch(ids, activations="f32" if ftype != "f32" else "q8")
+    c = np.sum(got * ref, axis=1)
+    print(arch, ftype, "oracle vs torch min cosine", c.min())
+    assert np.all(c >= 1 - 1e-4), c

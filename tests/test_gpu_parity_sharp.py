@@ -226,3 +226,26 @@ def test_q8_activation_envelope_c4(tmp_path, qk):
     if qk <= 0.03:
         assert np.all(c_hf >= 1 - 1e-4), c_hf
     assert np.all(c_hf >= c_qf), (c_hf, c_qf)
+
+
+def test_c3_hip_vs_torch_f32_activations(tmp_path):
+    """An independent cross-check of the HIP path that does not go through the oracle:
+    C3's architecture (bge-base, q4_0, sharp weights) against transformers' BertModel
+    on the file's dequantized weights with f32 activations (tests/test_cpu_oracle.py
+    _torch_forward: era constants, masked mean pool, L2 norm), ragged lengths up to
+    512.  The HIP path (f16 activations) tracks that f32-activation forward to 1e-4 in
+    cosine; the fp16-table GELU / exp of the reference's era are the
+    only other differences."""
+    import torch
+    from test_cpu_oracle import _model_tensors, _torch_forward
+    torch.set_num_threads(N_THR)
+    path = str(tmp_path / "bge-base-q4_0-sharp.bin")
+    bertpy.synthetic_model(path, "bge-base-en-v1.5", "q4_0", seed=1234, profile="sharp")
+    lens = [512, 3, 77, 300, 512, 129]
+    ids = bertpy.synthetic_ids(len(lens), lens, 30522, seed=17)
+    hip = bertpy.BertModel(path).forward_batch(ids)
+    hp, tensors = _model_tensors(oracle_lib, path)
+    ref = _torch_forward(hp, tensors, ids)
+    c = cosines(hip, ref)
+    record("C3-dims-q4_0-hip_vs_torch_f32", c)
+    assert np.all(c >= 1 - 1e-4), c
