@@ -228,24 +228,33 @@ def test_q8_activation_envelope_c4(tmp_path, qk):
     assert np.all(c_hf >= c_qf), (c_hf, c_qf)
 
 
-def test_c3_hip_vs_torch_f32_activations(tmp_path):
+TORCH_CONFIGS = {
+    "C2-MiniLM-f16": ("all-MiniLM-L6-v2", "f16", [128, 128, 3, 77]),
+    "C3-bge-base-q4_0": ("bge-base-en-v1.5", "q4_0", [512, 3, 77, 300, 512, 129]),
+    "C4-bge-large-q4_1": ("bge-large-en-v1.5", "q4_1", [512, 3, 200]),
+    "C5-bge-base-zh-q8_0": ("bge-base-zh-v1.5", "q8_0", [16, 511, 250, 90]),
+}
+
+
+@pytest.mark.parametrize("cfg", list(TORCH_CONFIGS))
+def test_hip_vs_torch_f32_activations(tmp_path, cfg):
     """An independent cross-check of the HIP path that does not go through the oracle:
-    C3's architecture (bge-base, q4_0, sharp weights) against transformers' BertModel
-    on the file's dequantized weights with f32 activations (tests/test_cpu_oracle.py
-    _torch_forward: era constants, masked mean pool, L2 norm), ragged lengths up to
-    512.  The HIP path (f16 activations) tracks that f32-activation forward to 1e-4 in
-    cosine; the fp16-table GELU / exp of the reference's era are the
-    only other differences."""
+    each SURVEY architecture and weight format on sharp weights against
+    transformers' BertModel on the file's dequantized weights with f32 activations
+    (tests/test_cpu_oracle.py _torch_forward: era constants, masked mean pool, L2
+    norm), ragged lengths up to 512.  The HIP path (f16 activations) tracks that
+    f32-activation forward to 1e-4 in cosine."""
     import torch
     from test_cpu_oracle import _model_tensors, _torch_forward
     torch.set_num_threads(N_THR)
-    path = str(tmp_path / "bge-base-q4_0-sharp.bin")
-    bertpy.synthetic_model(path, "bge-base-en-v1.5", "q4_0", seed=1234, profile="sharp")
-    lens = [512, 3, 77, 300, 512, 129]
-    ids = bertpy.synthetic_ids(len(lens), lens, 30522, seed=17)
+    arch, ftype, lens = TORCH_CONFIGS[cfg]
+    hp_arch = bertpy.ARCHS[arch]
+    path = str(tmp_path / f"{arch}-{ftype}-sharp.bin")
+    bertpy.synthetic_model(path, arch, ftype, seed=1234, profile="sharp")
+    ids = bertpy.synthetic_ids(len(lens), lens, hp_arch["n_vocab"], seed=17)
     hip = bertpy.BertModel(path).forward_batch(ids)
     hp, tensors = _model_tensors(oracle_lib, path)
     ref = _torch_forward(hp, tensors, ids)
     c = cosines(hip, ref)
-    record("C3-dims-q4_0-hip_vs_torch_f32", c)
+    record(f"{cfg}-hip_vs_torch_f32", c)
     assert np.all(c >= 1 - 1e-4), c
