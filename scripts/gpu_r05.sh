@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-5 GPU session.  STEPS selects (test bench prof pmc rehearsal b1trace
+# Round-5 GPU session.  STEPS selects (test smoke bench prof pmc rehearsal b1trace
 # envelope stamps share tok),
 # TAG names gpurun_out/<TAG>.  Every GPU step has its own limit; a fault, abort or
 # time limit ends the script.
@@ -17,6 +17,10 @@ if has test; then
   rc=$?
   tail -3 $OUT/gputest.log
   [ $rc -eq 0 ] || [ $rc -eq 1 ] || { tail -40 $OUT/gputest.log; exit 1; }
+fi
+if has smoke; then
+  step 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -20 $OUT/smoke.log; exit 1; }
+  tail -1 $OUT/smoke.log
 fi
 if has bench; then
   step 400 python -u bench.py ${BENCH_ARGS:-} > $OUT/bench.log 2>&1 || { tail -20 $OUT/bench.log; exit 1; }
