@@ -730,22 +730,10 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
                             pw[e] = __builtin_bit_cast(uint32_t, h16x2{(h16)v[a][2 * e], (h16)v[a][2 * e + 1]});
                     }
                     h16 *const dst = (h16 *)out + (size_t)tok * N + cb + 16 * a;
-                    typedef uint32_t u32x4n __attribute__((ext_vector_type(4)));
-                    if (ln.store_nt >= 2) {
-                        // write-through stores that drop the line from the XCD's L2
-                        // (cache policy sc1, 2: or sc0 sc1, 3; MI355X_MICROARCH.md
-                        // store flavours): the output does not evict the X panels and
-                        // weights the XCD's next tiles read
-                        const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
-                            (void *)((h16 *)out + (size_t)m0 * N), (short)0, BM * N * 2, 0x00020000);
-                        const int vo = ((tok - m0) * N + cb + 16 * a) * 2;
-                        if (ln.store_nt == 2) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4n, pk), ors, vo, 0, 16);
-                        else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4n, pk), ors, vo, 0, 17);
-                    } else if (ln.store_nt) {
-                        __builtin_nontemporal_store(__builtin_bit_cast(u32x4n, pk), (u32x4n *)dst);
-                    } else {
-                        *(uint4 *)dst = pk;
-                    }
+                    // plain stores: the next kernel reads the output from L2
+                    // (nt / write-through policies measured -18..-22 % on the C3
+                    // forward, profiles/r05i_gemm_store_policy_ab.log)
+                    *(uint4 *)dst = pk;
                 }
             }
         }
@@ -856,7 +844,6 @@ int launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, i
         // (gemm_fold_ok); anything else is an error, never a silent fallback
         if (!lnf || epi == EPI_BIAS_RES || ln.in_G <= 0 || ln.in_G > fold_cap(cfg) || 32 * ln.in_G != (W.kx ? W.kx : W.K))
             return -1;
-        if (ln.store_nt < 0) ln.store_nt = 0;
         switch (cfg) {
         case 3: dispatch_z<FMT, 4, 128, 4, 1, 3, 1, 0, 2, 12>(W, x, M, bias, epi, res, out, s, ln, lnf); break;
         case 16: dispatch_z<FMT, 4, 64, 4, 1, 3, 2, 3, 2, 24>(W, x, M, bias, epi, res, out, s, ln, lnf); break;
@@ -864,15 +851,6 @@ int launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, i
         }
         return cfg;
     }
-    // Non-temporal output stores on the 256-row tiles (large batches): the output
-    // streams past L2 instead of evicting the X panels the next column tiles read
-    // (C3: FFN-down 143 -> 140 us, QKV -1 us, forward +0.5 % alternating on one box,
-    // profiles/r03_attention_flow_ab.log nt rows; noise on another, r03_gemm_w8_nt_ab.log);
-    // the small forms keep L2
-    // stores (their next kernel reads the output while it is still there).
-    // BERT_GEMM_NT = 0 / 1 forces it off / on everywhere; 2 / 3: write-through
-    // stores with cache policy sc1 / sc0 sc1 (A/B).
-    if (ln.store_nt < 0) ln.store_nt = (cfg == 2 || cfg == 11) ? 1 : 0;
     // 256 x 128: the X pieces among the MFMAs (one per B-fragment item from the
     // K-step's start; +1.2-1.6 % on the C3 forward over one burst in front of them,
     // profiles/r03_gemm_xi_ab.log); cfg 11 keeps the burst form for A/B
@@ -942,9 +920,7 @@ int launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *b
     if (epi != EPI_BIAS_RES && (ln.in_stats || ln.in_part) && !ln.c1) return -1;
     if (ln.in_stats && ln.in_part) return -1;
     const bool lnf = epi == EPI_BIAS_RES ? res_ln : (ln.in_stats || ln.in_part);
-    static const int nt_env = [] { const char *e = std::getenv("BERT_GEMM_NT"); return e ? std::atoi(e) : -1; }();
-    LnFold lnx = ln;
-    lnx.store_nt = nt_env;
+    const LnFold lnx = ln;
     const int cfg = forward_cfg();
     switch (W.fmt) {
     case FMT_Q4_0: g_gemm_ran = launch_fmt<FMT_Q4_0>(W, x, M, bias, epi, res, out, s, lnx, lnf, cfg); break;

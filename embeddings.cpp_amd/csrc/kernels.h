@@ -91,9 +91,6 @@ struct LnFold {
     const float *g_next = nullptr;
     float2 *part = nullptr;
     int32_t part_stride = 0;
-    // output stores: -1 by tile config (launch_gemm); 0 plain, 1 non-temporal,
-    // 2 / 3 write-through with cache policy sc1 / sc0 sc1 (A/B)
-    int32_t store_nt = -1;
 };
 
 // Y[m][n] = epi( sum_k X[m][k] W[n][k] ), X f16 [M][K] with M % 64 == 0 (tiles of

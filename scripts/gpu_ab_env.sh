@@ -8,8 +8,9 @@ OUT=gpurun_out/${TAG:-ab}
 mkdir -p $OUT
 for r in 1 2; do
   for v in $VALS; do
-    env $VAR=$v timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-probes --no-library ${BENCH_ARGS:-} > $OUT/run_${v}_${r}.log 2>&1 || { tail -20 $OUT/run_${v}_${r}.log; exit 1; }
-    python3 - "$OUT/run_${v}_${r}.log" "$VAR=$v" <<'PY' | tee -a $OUT/ab.log
+    lg=$OUT/run_${v//\//_}_${r}.log
+    env $VAR=$v timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-probes --no-library ${BENCH_ARGS:-} > $lg 2>&1 || { tail -20 $lg; exit 1; }
+    python3 - "$lg" "$VAR=$v" <<'PY' | tee -a $OUT/ab.log
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 k = {n: round(v["avg_us"], 1) for n, v in d["kernels"].items()}

@@ -2,6 +2,7 @@
 and of the C oracle, as standalone programs built by tests/sanitize/Makefile (SURVEY §5:
 sanitizers on host code only; GPU sanitizers are unavailable on this pool).  Each run
 must exit 0 with no sanitizer report and give the same results as the production build."""
+import fcntl
 import os
 import random
 import struct
@@ -20,7 +21,11 @@ ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:halt_on_err
 
 @pytest.fixture(scope="module")
 def harness():
-    r = subprocess.run(["make", "-s", "-C", SAN, "-j2"], capture_output=True, text=True)
+    # one build at a time: pytest-xdist workers each run this fixture, and a worker
+    # must not exec a harness another worker's make is still linking
+    with open(os.path.join(SAN, ".build.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        r = subprocess.run(["make", "-s", "-C", SAN, "-j2"], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-3000:]
     return os.path.join(SAN, "_build")
 
