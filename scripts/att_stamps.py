@@ -12,7 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "embeddings.cpp_amd"))
 import bertpy  # noqa: E402
 
-L = bertpy.load_lib(os.path.join(ROOT, "build", "stamps", "libbert.so"))
+L = bertpy.load_lib(os.environ.get("STAMPS_LIB") or os.path.join(ROOT, "build", "stamps", "libbert.so"))
 us = ctypes.c_float()
 assert L.bertx_bench_attention(64, 512, 12, 64, int(os.environ.get("ATT_VARIANT", "0")), 20, ctypes.byref(us)) == 0
 n = 1 << 17
