@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-5 GPU session.  STEPS selects (test smoke bench prof pmc rehearsal b1trace
-# envelope stamps share tok),
+# c2trace envelope stamps share tok),
 # TAG names gpurun_out/<TAG>.  Every GPU step has its own limit; a fault, abort or
 # time limit ends the script.
 set -o pipefail
@@ -43,6 +43,10 @@ fi
 if has b1trace; then
   # GPU-side kernel durations of the B = 1, L = 32 forward (graph replay)
   ( cd /tmp && step 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/b1prof -o b1 --output-format csv -- python3 $GRAFT_REPO_ROOT/scripts/b1_trace.py 32 200 > $GRAFT_REPO_ROOT/$OUT/b1trace.log 2>&1 ) || { tail -20 $OUT/b1trace.log; exit 1; }
+fi
+if has c2trace; then
+  # GPU-side kernel durations of the C2 forward (MiniLM f16, B 32, L 128, graph replay)
+  ( cd /tmp && step 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/c2prof -o c2 --output-format csv -- python3 $GRAFT_REPO_ROOT/scripts/b1_trace.py 128 200 32 all-MiniLM-L6-v2 f16 > $GRAFT_REPO_ROOT/$OUT/c2trace.log 2>&1 ) || { tail -20 $OUT/c2trace.log; exit 1; }
 fi
 if has envelope; then
   step 600 python -u scripts/q8_envelope.py --out $OUT/q8_envelope.jsonl > $OUT/envelope.log 2>&1 || { tail -20 $OUT/envelope.log; exit 1; }
