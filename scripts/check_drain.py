@@ -5,8 +5,9 @@ in flight into a register the compiler reuses in the epilogue.
 
 Extracts the gfx950 code objects from build/libbert.so (clang offload bundles in
 .hip_fatbin), disassembles every GEMM / attention kernel, and checks that on every
-straight-line path from the last LDS read of the K loop to the first global / buffer
-store of the epilogue there is an `s_waitcnt` with lgkmcnt(0).  Usage:
+straight-line path from the last LDS read of the K loop (the last one ahead of the
+last MFMA before the first store) to the first global / buffer store of the epilogue
+there is an `s_waitcnt` with lgkmcnt(0).  Usage:
   scripts/check_drain.py [libbert.so]        -> prints one line per kernel, rc 1 on a miss
 """
 import os
@@ -65,13 +66,20 @@ def lgkm_zero(ins):
 
 
 def check(body):
-    """None if every LDS read before the first store is drained by an lgkmcnt(0) wait
-    placed after it and before that store, else a description of the miss."""
+    """None if the K loop's last LDS read is drained by an lgkmcnt(0) wait placed after
+    it and before the first store, else a description of the miss.  The K loop's reads
+    (the asm ones among them) all feed MFMAs, so they come before the last MFMA ahead of
+    the first store; LDS reads the compiler schedules after that MFMA are the
+    epilogue's own (bias, LN parameters, row statistics), which hipcc waits for itself."""
     first_store = next((i for i, s in enumerate(body) if re.match(r"(global|buffer)_store", s)), None)
     if first_store is None:
         return None
-    last_read = None
+    last_mfma = None
     for i in range(first_store):
+        if "mfma" in body[i]:
+            last_mfma = i
+    last_read = None
+    for i in range(last_mfma if last_mfma is not None else first_store):
         if body[i].startswith("ds_read"):
             last_read = i
     if last_read is None:
