@@ -304,7 +304,9 @@ def probes(lib, bertpy, torch, a, dev, stream, q4_path):
         -- forward latency and algorithmic bytes (weights at stored width + rows +
         ids + output) / latency against 8 TB/s, and this run's counter bytes (pmc_live)
         / latency beside it.  The probe always builds bge-base-en-v1.5 q4_0, whatever
-        --arch/--ftype the headline runs."""
+        --arch/--ftype the headline runs;
+      c4_shard / c5_ragged: BASELINE.json's C4 at one GPU's share and C5 -- sentences/s,
+        tokens/s and the dominant kernel."""
     out = {}
     steps = max(a.steps, 20)
     # C2
@@ -368,6 +370,39 @@ def probes(lib, bertpy, torch, a, dev, stream, q4_path):
         except Exception as ex:
             out["q4_0_hbm"]["pmc"] = {"error": str(ex)}
     del f
+    # the other two GPU configs of BASELINE.json at one GPU's share: C4 (bge-large q4_1,
+    # L 512, 256 sentences over 8 GPUs = 32 per GPU: the replicas-only multi-GPU
+    # path runs exactly this per GPU) and C5 (bge-base-zh q8_0, 128 ragged sentences)
+    import numpy as np
+    rng = np.random.default_rng(11)
+    for key, arch, ftype, lens, what in (
+            ("c4_shard", "bge-large-en-v1.5", "q4_1", [512] * 32,
+             "C4 per GPU: bge-large-en-v1.5 q4_1, L 512, 32 sentences (256 over 8 GPUs as replicas)"),
+            ("c5_ragged", "bge-base-zh-v1.5", "q8_0", [int(x) for x in rng.integers(16, 513, 128)],
+             "C5: bge-base-zh-v1.5 q8_0, 128 sentences, lengths uniform in [16, 512] (seed 11)")):
+        try:
+            hp = bertpy.ARCHS[arch]
+            pth = ensure_model(bertpy, a.model_dir, arch, ftype, a.seed)
+            f = DeviceForward(lib, bertpy, torch, pth, bertpy.synthetic_ids(len(lens), lens, hp["n_vocab"], seed=7),
+                              dev, stream)
+            for _ in range(3):
+                f.step()
+            f.sync()
+            f.check()
+            n = max(5, min(steps, 20))
+            el = timed_steps(f.step, n, f.sync)
+            _, st = f.kernel_pass(n)
+            name, avg_s, work, is_flops = dominant(st)
+            rec = {"workload": what, "sentences_per_s": round(len(lens) * n / el, 1),
+                   "tokens_per_s": round(sum(lens) * n / el, 0), "ms_per_batch": round(el / n * 1e3, 4),
+                   "dominant_kernel": name, "avg_launch_us": round(avg_s * 1e6, 2)}
+            if is_flops:
+                ach = work / avg_s / 1e12
+                rec.update({"achieved_tflops": round(ach, 1), "mfma_frac": round(ach / MFMA_F16_PEAK_TFLOPS, 4)})
+            out[key] = rec
+            del f
+        except Exception as ex:   # a probe is a report, never the metric
+            out[key] = {"error": str(ex)}
     return out
 
 
