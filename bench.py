@@ -227,6 +227,11 @@ def pmc_pass(model_path, B, L, counter, steps, warmup, timeout_s, device):
     out = tempfile.mkdtemp(prefix="bench_pmc_", dir="/tmp")
     try:
         env = dict(os.environ, BERT_GRAPHS="0", BERT_DEVICES=str(device), TMPDIR="/tmp")
+        if os.environ.get("BERT_LIB"):
+            # A/B runs against another build: the probe's RUNPATH ($ORIGIN/..) would
+            # load build/libbert.so; LD_LIBRARY_PATH is searched before a RUNPATH
+            lp = os.path.dirname(os.path.abspath(os.environ["BERT_LIB"]))
+            env["LD_LIBRARY_PATH"] = lp + (":" + env["LD_LIBRARY_PATH"] if env.get("LD_LIBRARY_PATH") else "")
         cmd = ["timeout", "-s", "KILL", str(timeout_s), rp, "--pmc", counter, "--output-format", "csv",
                "-d", out, "-o", "pmc", "--", PROBE_BIN, model_path, str(B), str(L), str(steps), str(warmup)]
         r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
