@@ -20,7 +20,9 @@
 #include <functional>
 #include <memory>
 #include <numeric>
+#include <stdexcept>
 #include <string>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -65,7 +67,7 @@ private:
             }
             // nothing may leave the worker thread (std::terminate); run_forward's
             // tasks catch their own failures, this is the last line
-            try { f(); } catch (...) { std::fprintf(stderr, "libbert: replica worker task failed\n"); }
+            try { f(); } catch (...) { emb::errorf("libbert: replica worker task failed\n"); }
         }
     }
     std::mutex mu_;
@@ -149,7 +151,7 @@ double sentence_cost(const emb::HParams &hp, int L)
 int run_forward(bert_ctx *ctx, const int32_t *const *toks, const int32_t *lens, float *const *outs, int n)
 {
     if (ctx->devices.empty()) {
-        std::fprintf(stderr, "libbert: no HIP device in this context (BERT_HOST_ONLY); forward unavailable\n");
+        emb::errorf("libbert: no HIP device in this context (BERT_HOST_ONLY); forward unavailable\n");
         return -1;
     }
     if (n <= 0) return 0;
@@ -228,10 +230,10 @@ int run_forward(bert_ctx *ctx, const int32_t *const *toks, const int32_t *lens, 
         try {
             work(dv);
         } catch (const std::exception &ex) {
-            std::fprintf(stderr, "libbert: replica %d share failed: %s\n", dv, ex.what());
+            emb::errorf("libbert: replica %d share failed: %s\n", dv, ex.what());
             rcs[(size_t)dv] = -1;
         } catch (...) {
-            std::fprintf(stderr, "libbert: replica %d share failed\n", dv);
+            emb::errorf("libbert: replica %d share failed\n", dv);
             rcs[(size_t)dv] = -1;
         }
         finish(dv);
@@ -272,7 +274,7 @@ int run_forward(bert_ctx *ctx, const int32_t *const *toks, const int32_t *lens, 
         cv.wait(lk, [&] { return left == 0; });
     }
     for (int rc : rcs) if (rc != 0) {
-        std::fprintf(stderr, "libbert: forward failed (%d)\n", rc);
+        emb::errorf("libbert: forward failed (%d)\n", rc);
         return rc;
     }
     return 0;
@@ -295,10 +297,10 @@ bool tokenize_all(const bert_ctx *ctx, int n_threads, int n, const char *const *
                 lens[i] = ctx->vocab.tokenize(texts[i], n_max, ids + (size_t)i * n_max, n_max);
         });
     } catch (const std::exception &ex) {
-        std::fprintf(stderr, "libbert: tokenization failed: %s\n", ex.what());
+        emb::errorf("libbert: tokenization failed: %s\n", ex.what());
         return false;
     } catch (...) {
-        std::fprintf(stderr, "libbert: tokenization failed\n");
+        emb::errorf("libbert: tokenization failed\n");
         return false;
     }
     return true;
@@ -353,53 +355,88 @@ bool bert_params_parse(int argc, char **argv, bert_params &params)
     return true;
 }
 
-struct bert_ctx *bert_load_from_file(const char *fname)
+// The reference's loader reports and returns nullptr on every failure
+// (bert.cpp:423-443, 684-750); so does this one: nothing thrown inside (a
+// bad_alloc of the host repack, a std::system_error starting a worker thread)
+// leaves the C ABI, and every partly built replica is released on the way out.
+// All HIP calls of the load run on this thread, one replica after another; the
+// weight uploads still overlap (async copies from one page-locked image on each
+// replica's stream).  DESIGN §11 has the round-5 abort this replaces.
+static bert_ctx *load_context(const char *fname)
 {
-    std::printf("bert_load_from_file: loading model from '%s' - please wait ...\n", fname);
+    emb::infof("bert_load_from_file: loading model from '%s' - please wait ...\n", fname);
+    if (emb::fault_inject("load")) throw std::runtime_error("BERT_FAULT_INJECT=load");
     emb::HostModel m;
     std::string err;
     if (!emb::load_model_file(fname, m, err, true)) {
-        std::fprintf(stderr, "bert_load_from_file: %s\n", err.c_str());
+        emb::errorf("bert_load_from_file: %s\n", err.c_str());
         return nullptr;
     }
+    // declared before ctx: on a failure the replicas (ctx) are released first, and
+    // each waits for its upload from the page-locked image before the image goes
+    emb::ModelImage img;
     std::unique_ptr<bert_ctx> ctx(new bert_ctx);
     ctx->hp = m.hp;
     ctx->vocab.build(m.vocab);
     const char *ho = std::getenv("BERT_HOST_ONLY");
     const bool host_only = ho && *ho && std::strcmp(ho, "0") != 0;
-    const std::vector<int> devs = host_only ? std::vector<int>() : parse_device_list(emb::hip_device_count());
-    if (devs.empty()) {
-        if (!host_only) {
-            std::fprintf(stderr, "bert_load_from_file: no HIP (gfx950) device available -- libbert.so has no CPU "
-                                 "compute path (set BERT_HOST_ONLY=1 for a tokenizer-only context)\n");
-            return nullptr;
-        }
+    if (host_only) {
         ctx->host_only = true;
-        std::printf("bert_load_from_file: host-only context (tokenizer only, no forward)\n");
+        emb::infof("bert_load_from_file: host-only context (tokenizer only, no forward)\n");
         return ctx.release();
     }
-    std::vector<std::unique_ptr<Device>> made(devs.size());
-    {
-        std::vector<std::thread> th;
-        for (size_t i = 0; i < devs.size(); ++i)
-            th.emplace_back([&, i] { made[i].reset(new Device(devs[i], m)); });
-        for (auto &t : th) t.join();
+    const std::vector<int> devs = parse_device_list(emb::hip_device_count());
+    // the host half of the load, once for all replicas: repack into one image
+    emb::trace("bert_load_from_file: building the device image\n");
+    if (!emb::build_model_image(m, img, err, !devs.empty())) {
+        emb::errorf("bert_load_from_file: %s\n", err.c_str());
+        return nullptr;
     }
-    for (auto &d : made) {
-        if (!d->ok()) {
-            std::fprintf(stderr, "bert_load_from_file: device %d initialisation failed\n", d->ordinal());
-            return nullptr;
+    emb::trace("bert_load_from_file: image %zu bytes (%s)\n", img.total, img.pinned() ? "page-locked" : "pageable");
+    { emb::HostModel none; std::swap(m.layers, none.layers); }   // the file tensors are no longer needed
+    if (devs.empty()) {
+        emb::errorf("bert_load_from_file: no HIP (gfx950) device available -- libbert.so has no CPU "
+                    "compute path (set BERT_HOST_ONLY=1 for a tokenizer-only context)\n");
+        return nullptr;
+    }
+    for (size_t i = 0; i < devs.size(); ++i) {
+        emb::trace("bert_load_from_file: replica %zu on device %d: create + upload\n", i, devs[i]);
+        if (i == 1 && emb::fault_inject("replica1")) throw std::runtime_error("BERT_FAULT_INJECT=replica1");
+        ctx->devices.emplace_back(new Device(devs[i], img));
+    }
+    bool ok = true;
+    for (auto &d : ctx->devices) {
+        if (!d->finish_load()) {
+            emb::errorf("bert_load_from_file: device %d initialisation failed\n", d->ordinal());
+            ok = false;
         }
-        ctx->devices.push_back(std::move(d));
     }
+    if (!ok) return nullptr;
+    emb::trace("bert_load_from_file: %zu replica(s) uploaded\n", ctx->devices.size());
     ctx->inflight.assign(ctx->devices.size(), 0.0);
-    if (ctx->devices.size() > 1)
+    if (ctx->devices.size() > 1) {
+        if (emb::fault_inject("worker")) throw std::system_error(std::make_error_code(std::errc::resource_unavailable_try_again), "BERT_FAULT_INJECT=worker");
         for (size_t i = 0; i < ctx->devices.size(); ++i) ctx->workers.emplace_back(new ReplicaWorker());
-    std::printf("bert_load_from_file: MI355X engine on %zu HIP device(s)\n", ctx->devices.size());
+    }
+    emb::infof("bert_load_from_file: MI355X engine on %zu HIP device(s)\n", ctx->devices.size());
     if (m.hp.ftype == emb::FMT_F32)
-        std::printf("bert_load_from_file: f32 file: f32 activations x f32 weights on the f32 MFMA chain "
-                    "(as the reference multiplies them, bert.cpp:499-503)\n");
+        emb::infof("bert_load_from_file: f32 file: f32 activations x f32 weights on the f32 MFMA chain "
+                   "(as the reference multiplies them, bert.cpp:499-503)\n");
     return ctx.release();
+}
+
+struct bert_ctx *bert_load_from_file(const char *fname)
+{
+    try {
+        return load_context(fname);
+    } catch (const std::bad_alloc &) {
+        emb::errorf("bert_load_from_file: out of host memory\n");
+    } catch (const std::exception &ex) {
+        emb::errorf("bert_load_from_file: load failed: %s\n", ex.what());
+    } catch (...) {
+        emb::errorf("bert_load_from_file: load failed\n");
+    }
+    return nullptr;
 }
 
 void bert_free(bert_ctx *ctx) { delete ctx; }
@@ -422,7 +459,7 @@ void bert_forward_batch(bert_ctx *ctx, int32_t n_threads, int32_t n_batch_size, 
     int32_t mx = 0;
     for (int i = 0; i < n_batch_size; ++i) mx = std::max(mx, n_tokens[i]);
     if (mx > ctx->hp.n_max_tokens) {
-        std::fprintf(stderr, "Too many tokens, maximum is %d\n", ctx->hp.n_max_tokens);
+        emb::errorf("Too many tokens, maximum is %d\n", ctx->hp.n_max_tokens);
         return;
     }
     run_forward(ctx, batch_tokens, n_tokens, batch_embeddings, n_batch_size);
@@ -443,7 +480,7 @@ void bert_forward_fake_batch(bert_ctx *ctx, int32_t n_threads, int32_t n_batch_s
     int n_ok = 0;
     while (n_ok < n_batch_size && n_tokens[n_ok] <= ctx->hp.n_max_tokens) ++n_ok;
     run_forward(ctx, batch_tokens, n_tokens, batch_embeddings, n_ok);
-    if (n_ok < n_batch_size) std::fprintf(stderr, "Too many tokens, maximum is %d\n", ctx->hp.n_max_tokens);
+    if (n_ok < n_batch_size) emb::errorf("Too many tokens, maximum is %d\n", ctx->hp.n_max_tokens);
 }
 
 void bert_encode_batch(struct bert_ctx *ctx, int32_t n_threads, int32_t n_batch_size, int32_t n_inputs,
@@ -458,7 +495,7 @@ void bert_encode_batch(struct bert_ctx *ctx, int32_t n_threads, int32_t n_batch_
     std::vector<char> ok((size_t)n_inputs, 1);
     if (n_batch_size == n_inputs || n_batch_size <= 0) {
         if (*std::max_element(lens.begin(), lens.end()) > N) {
-            std::fprintf(stderr, "Too many tokens, maximum is %d\n", N);
+            emb::errorf("Too many tokens, maximum is %d\n", N);
             return;
         }
     } else {
@@ -468,7 +505,7 @@ void bert_encode_batch(struct bert_ctx *ctx, int32_t n_threads, int32_t n_batch_
         for (int s = 0; s < n_inputs; s += n_batch_size) {
             const int e = std::min(n_inputs, s + n_batch_size);
             if (lens[(size_t)idx[(size_t)e - 1]] > N) {
-                std::fprintf(stderr, "Too many tokens, maximum is %d\n", N);
+                emb::errorf("Too many tokens, maximum is %d\n", N);
                 for (int j = s; j < e; ++j) ok[(size_t)idx[(size_t)j]] = 0;
             }
         }

@@ -200,7 +200,7 @@ bool load_safetensors(const std::string &path, std::map<std::string, StTensor> &
 {
     std::string raw;
     if (!read_file(path, raw) || raw.size() < 8) {
-        std::fprintf(stderr, "convert: cannot read '%s'\n", path.c_str());
+        errorf("convert: cannot read '%s'\n", path.c_str());
         return false;
     }
     uint64_t hlen;
@@ -208,7 +208,7 @@ bool load_safetensors(const std::string &path, std::map<std::string, StTensor> &
     if (hlen > raw.size() - 8) return false;
     JVal hdr;
     if (!parse_json(raw.substr(8, hlen), hdr)) {
-        std::fprintf(stderr, "convert: bad safetensors header in '%s'\n", path.c_str());
+        errorf("convert: bad safetensors header in '%s'\n", path.c_str());
         return false;
     }
     const char *base = raw.data() + 8 + hlen;
@@ -229,7 +229,7 @@ bool load_safetensors(const std::string &path, std::map<std::string, StTensor> &
         else if (dt->str == "F16" || dt->str == "BF16") esz = 2;
         else if (dt->str == "F64") esz = 8;
         else {
-            std::fprintf(stderr, "convert: tensor '%s' has unsupported dtype %s\n", kv.first.c_str(),
+            errorf("convert: tensor '%s' has unsupported dtype %s\n", kv.first.c_str(),
                          dt->str.c_str());
             return false;
         }
@@ -286,13 +286,13 @@ template <typename T> void put(std::string &o, const T &v) { o.append((const cha
 int convert_hf_dir(const std::string &dir, const std::string &fname_out, int ftype)
 {
     if (ftype < 0 || ftype > 1) {
-        std::fprintf(stderr, "Invalid ftype: %d\n", ftype);
+        errorf("Invalid ftype: %d\n", ftype);
         return 1;
     }
     std::string s;
     JVal cfg;
     if (!read_file(dir + "/config.json", s) || !parse_json(s, cfg)) {
-        std::fprintf(stderr, "convert: cannot read %s/config.json\n", dir.c_str());
+        errorf("convert: cannot read %s/config.json\n", dir.c_str());
         return 1;
     }
     const char *keys[] = {"vocab_size", "max_position_embeddings", "hidden_size", "intermediate_size",
@@ -301,7 +301,7 @@ int convert_hf_dir(const std::string &dir, const std::string &fname_out, int fty
     for (int i = 0; i < 6; ++i) {
         const JVal *v = cfg.get(keys[i]);
         if (!v || v->kind != JVal::NUM) {
-            std::fprintf(stderr, "convert: config.json lacks %s\n", keys[i]);
+            errorf("convert: config.json lacks %s\n", keys[i]);
             return 1;
         }
         hp[i] = (int32_t)v->num;
@@ -309,7 +309,7 @@ int convert_hf_dir(const std::string &dir, const std::string &fname_out, int fty
 
     // vocab.txt in text mode: universal newlines, each line keeps its "\n"
     if (!read_file(dir + "/vocab.txt", s)) {
-        std::fprintf(stderr, "convert: cannot read %s/vocab.txt\n", dir.c_str());
+        errorf("convert: cannot read %s/vocab.txt\n", dir.c_str());
         return 1;
     }
     std::vector<std::string> lines;
@@ -326,7 +326,7 @@ int convert_hf_dir(const std::string &dir, const std::string &fname_out, int fty
         if (!cur.empty()) lines.push_back(cur);
     }
     if ((int64_t)lines.size() < hp[0]) {
-        std::fprintf(stderr, "convert: vocab.txt has %zu lines, config says vocab_size %d\n", lines.size(), hp[0]);
+        errorf("convert: vocab.txt has %zu lines, config says vocab_size %d\n", lines.size(), hp[0]);
         return 1;
     }
 
@@ -342,7 +342,7 @@ int convert_hf_dir(const std::string &dir, const std::string &fname_out, int fty
         for (auto &f : shards)
             if (!load_safetensors(dir + "/" + f, raw)) return 1;
     } else if (!load_safetensors(dir + "/model.safetensors", raw)) {
-        std::fprintf(stderr, "convert: %s has no model.safetensors (pickled checkpoints are not read)\n",
+        errorf("convert: %s has no model.safetensors (pickled checkpoints are not read)\n",
                      dir.c_str());
         return 1;
     }
@@ -352,7 +352,7 @@ int convert_hf_dir(const std::string &dir, const std::string &fname_out, int fty
     std::vector<std::string> order = state_dict_order(hp[5]);
     for (auto &n : order)
         if (!byname.count(n)) {
-            std::fprintf(stderr, "convert: checkpoint lacks tensor '%s'\n", n.c_str());
+            errorf("convert: checkpoint lacks tensor '%s'\n", n.c_str());
             return 1;
         }
     // anything else BertModel would hold (not the pooler / position_ids / task heads)
@@ -392,7 +392,7 @@ int convert_hf_dir(const std::string &dir, const std::string &fname_out, int fty
     }
     FILE *f = std::fopen(fname_out.c_str(), "wb");
     if (!f) {
-        std::fprintf(stderr, "convert: cannot open '%s' for writing\n", fname_out.c_str());
+        errorf("convert: cannot open '%s' for writing\n", fname_out.c_str());
         return 1;
     }
     const bool ok = std::fwrite(o.data(), 1, o.size(), f) == o.size();

@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <new>
 
 namespace emb {
 
@@ -16,7 +17,7 @@ namespace emb {
     do {                                                                                                 \
         hipError_t e_ = (expr);                                                                          \
         if (e_ != hipSuccess) {                                                                          \
-            std::fprintf(stderr, "libbert: HIP error %s at %s:%d (%s)\n", hipGetErrorString(e_), __FILE__, \
+            errorf("libbert: HIP error %s at %s:%d (%s)\n", hipGetErrorString(e_), __FILE__, \
                          __LINE__, #expr);                                                               \
             return false;                                                                                \
         }                                                                                                \
@@ -26,7 +27,7 @@ namespace emb {
     do {                                                                                                 \
         hipError_t e_ = (expr);                                                                          \
         if (e_ != hipSuccess) {                                                                          \
-            std::fprintf(stderr, "libbert: HIP error %s at %s:%d (%s)\n", hipGetErrorString(e_), __FILE__, \
+            errorf("libbert: HIP error %s at %s:%d (%s)\n", hipGetErrorString(e_), __FILE__, \
                          __LINE__, #expr);                                                               \
             return -1;                                                                                   \
         }                                                                                                \
@@ -215,20 +216,199 @@ void repack_table(const HostTensor &t, Piece &qs, Piece &dpl, Piece &mpl)
 
 }  // namespace
 
-Device::Device(int ordinal, const HostModel &m) : ordinal_(ordinal), hp_(m.hp)
+ModelImage::~ModelImage()
+{
+    if (pinned_) (void)hipHostFree(pinned_);
+}
+
+bool build_model_image(const HostModel &m, ModelImage &img, std::string &err, bool pin)
+{
+    try {
+        const HParams &hp = m.hp;
+        const int d = hp.n_embd, f = hp.n_intermediate;
+        if (hp.n_head <= 0 || d % 64 || d > 1024 || f % 64 || (d / hp.n_head != 32 && d / hp.n_head != 64)) {
+            char buf[256];
+            std::snprintf(buf, sizeof buf,
+                          "unsupported shape n_embd=%d n_intermediate=%d n_head=%d (need n_embd %% 64 == 0, "
+                          "n_embd <= 1024, head_dim 32 or 64)", d, f, hp.n_head);
+            err = buf;
+            return false;
+        }
+        if (fault_inject("image")) throw std::bad_alloc();
+        img.hp = hp;
+        img.wfmt = hp.ftype;
+        // f32 files run the f32 chain (f32.hip) on the file's own f32 rows; the other
+        // formats the lane-order layout of the MFMA f16 GEMMs
+        img.f32 = img.wfmt == FMT_F32;
+        std::vector<Piece> pieces;
+        pieces.reserve(16 + 24 * (size_t)hp.n_layer);
+        auto add = [&](Piece &&p) -> size_t { pieces.push_back(std::move(p)); return pieces.size() - 1; };
+        auto vec = [&](const HostTensor &t) -> size_t { Piece p; p.bytes = t.bytes; return add(std::move(p)); };
+        auto table = [&](const HostTensor &t) -> ModelImage::Tab {
+            Piece q, dd, mm;
+            repack_table(t, q, dd, mm);
+            ModelImage::Tab r;
+            r.fmt = t.fmt; r.rows = t.ne1; r.cols = t.ne0;
+            r.q = add(std::move(q)); r.d = add(std::move(dd)); r.m = add(std::move(mm));
+            return r;
+        };
+        auto linear = [&](std::vector<const HostTensor *> parts) -> ModelImage::Lin {
+            Piece q, dd, mm;
+            ModelImage::Lin r;
+            repack_linear(parts, img.wfmt, q, dd, mm, r.N, r.K);
+            r.q = add(std::move(q)); r.d = add(std::move(dd)); r.m = add(std::move(mm));
+            return r;
+        };
+        img.word = table(m.word);
+        img.type = table(m.ttype);
+        img.pos = table(m.pos);
+        // f32 chain: the era's fp16 GELU and exp tables, built on the host (libm) as
+        // ggml built them, indexed on the device by the f16 bits of the input
+        if (img.f32) {
+            std::vector<uint16_t> tg, te;
+            era_tables(tg, te);
+            Piece pg, pe;
+            pg.bytes.assign((const uint8_t *)tg.data(), (const uint8_t *)(tg.data() + tg.size()));
+            pe.bytes.assign((const uint8_t *)te.data(), (const uint8_t *)(te.data() + te.size()));
+            img.gelu = add(std::move(pg));
+            img.exp = add(std::move(pe));
+        }
+        img.lnw = vec(m.ln_e_w);
+        img.lnb = vec(m.ln_e_b);
+        auto fold = [&](std::vector<const HostTensor *> parts, std::vector<const HostTensor *> bias,
+                        const HostTensor &gamma, const HostTensor &beta, size_t &i1, size_t &i2) {
+            Piece c1, c2;
+            fold_ln(parts, bias, gamma, beta, c1, c2, img.wfmt == FMT_F32);
+            i1 = add(std::move(c1));
+            i2 = add(std::move(c2));
+        };
+        // f32 chain: the rows of the parts as f32 (concatenated along N)
+        auto rows32 = [&](std::vector<const HostTensor *> parts) -> size_t {
+            Piece p;
+            for (const HostTensor *t : parts) {
+                const size_t n0 = p.bytes.size();
+                p.bytes.resize(n0 + (size_t)t->ne1 * t->ne0 * 4);
+                for (int r = 0; r < t->ne1; ++r)
+                    dequant_row(t->fmt, t->bytes.data() + fmt_row_bytes(t->fmt, t->ne0) * r,
+                                (float *)(p.bytes.data() + n0) + (size_t)r * t->ne0, t->ne0);
+            }
+            return add(std::move(p));
+        };
+        img.layers.assign((size_t)hp.n_layer, ModelImage::Layer());
+        for (int l = 0; l < hp.n_layer; ++l) {
+            const HostLayer &L = m.layers[(size_t)l];
+            ModelImage::Layer &x = img.layers[(size_t)l];
+            if (img.f32) {
+                x.w32q = rows32({&L.q_w, &L.k_w, &L.v_w}); x.w32o = rows32({&L.o_w});
+                x.w32u = rows32({&L.i_w}); x.w32d = rows32({&L.o2_w});
+                x.bq = rows32({&L.q_b, &L.k_b, &L.v_b}); x.bu = vec(L.i_b);
+                x.bo = vec(L.o_b); x.bdown = vec(L.o2_b);
+                x.l1w = vec(L.ln_att_w); x.l1b = vec(L.ln_att_b); x.l2w = vec(L.ln_out_w); x.l2b = vec(L.ln_out_b);
+                continue;
+            }
+            x.qkv = linear({&L.q_w, &L.k_w, &L.v_w});
+            x.o = linear({&L.o_w});
+            x.up = linear({&L.i_w});
+            x.down = linear({&L.o2_w});
+            // the LN in front of QKV: the previous layer's output LN, or the embedding LN
+            const HostTensor &gq = l ? m.layers[(size_t)l - 1].ln_out_w : m.ln_e_w;
+            const HostTensor &bq = l ? m.layers[(size_t)l - 1].ln_out_b : m.ln_e_b;
+            fold({&L.q_w, &L.k_w, &L.v_w}, {&L.q_b, &L.k_b, &L.v_b}, gq, bq, x.c1q, x.c2q);
+            fold({&L.i_w}, {&L.i_b}, L.ln_att_w, L.ln_att_b, x.c1u, x.c2u);
+            x.bo = vec(L.o_b); x.bdown = vec(L.o2_b);
+            x.l1w = vec(L.ln_att_w); x.l1b = vec(L.ln_att_b); x.l2w = vec(L.ln_out_w); x.l2b = vec(L.ln_out_b);
+        }
+        img.off.resize(pieces.size());
+        img.len.resize(pieces.size());
+        size_t total = 0;
+        for (size_t i = 0; i < pieces.size(); ++i) {
+            img.off[i] = total;
+            img.len[i] = pieces[i].bytes.size();
+            total += align_up(pieces[i].bytes.size(), 256);
+        }
+        img.total = total ? total : 256;
+        // one contiguous image, page-locked when possible so each replica's upload is
+        // one async copy on its own stream; pieces are freed as they are copied
+        uint8_t *dst = nullptr;
+        if (pin) {
+            if (hipHostMalloc((void **)&img.pinned_, img.total, hipHostMallocDefault) != hipSuccess) {
+                (void)hipGetLastError();
+                img.pinned_ = nullptr;
+                trace("build_model_image: page-locking %zu bytes failed, pageable uploads\n", img.total);
+            }
+        }
+        if (img.pinned_) {
+            dst = img.pinned_;
+        } else {
+            img.host_.assign(img.total, 0);
+            dst = img.host_.data();
+        }
+        for (size_t i = 0; i < pieces.size(); ++i) {
+            Piece &p = pieces[i];
+            if (!p.bytes.empty()) std::memcpy(dst + img.off[i], p.bytes.data(), p.bytes.size());
+            const size_t pad = align_up(p.bytes.size(), 256) - p.bytes.size();
+            if (pad) std::memset(dst + img.off[i] + p.bytes.size(), 0, pad);
+            std::vector<uint8_t>().swap(p.bytes);
+        }
+        return true;
+    } catch (const std::bad_alloc &) {
+        err = "out of host memory building the device image";
+    } catch (const std::exception &ex) {
+        err = std::string("building the device image failed: ") + ex.what();
+    }
+    return false;
+}
+
+Device::Device(int ordinal, const ModelImage &img) : ordinal_(ordinal), hp_(img.hp)
 {
     DeviceGuard g(ordinal);
     if (!g.ok() || hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&done_ev_, hipEventDisableTiming) != hipSuccess) {
-        std::fprintf(stderr, "libbert: cannot initialise HIP device %d\n", ordinal);
+        (void)hipGetLastError();
+        errorf("libbert: cannot initialise HIP device %d\n", ordinal);
         return;
     }
-    upload(m);
+    if (hipMalloc((void **)&arena_, img.total) != hipSuccess) {
+        (void)hipGetLastError();
+        errorf("libbert: hipMalloc of %zu bytes of weights failed on device %d\n", img.total, ordinal_);
+        arena_ = nullptr;
+        return;
+    }
+    arena_size_ = img.total;
+    // page-locked image: one async copy on this replica's stream, so the uploads of
+    // all replicas overlap although one thread issues them; pageable: a blocking copy
+    const hipError_t e = img.pinned()
+        ? hipMemcpyAsync(arena_, img.bytes(), img.total, hipMemcpyHostToDevice, stream_)
+        : hipMemcpy(arena_, img.bytes(), img.total, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        errorf("libbert: weight upload failed on device %d: %s\n", ordinal_, hipGetErrorString(e));
+        return;
+    }
+    bind(img);
+    uploading_ = true;
+}
+
+bool Device::finish_load()
+{
+    if (!uploading_) return false;
+    DeviceGuard g(ordinal_);
+    if (!g.ok()) return false;
+    const hipError_t e = hipStreamSynchronize(stream_);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        errorf("libbert: weight upload failed on device %d: %s\n", ordinal_, hipGetErrorString(e));
+        return false;
+    }
+    uploading_ = false;
+    ok_ = true;
+    return true;
 }
 
 Device::~Device()
 {
     DeviceGuard g(ordinal_);
+    if (stream_ && uploading_) (void)hipStreamSynchronize(stream_);   // the image may still be in flight
     if (done_ev_ && any_forward_) (void)hipEventSynchronize(done_ev_);
     if (stream_) (void)hipStreamSynchronize(stream_);
     drop_graphs();
@@ -255,140 +435,38 @@ void Device::mark_done(hipStream_t s)
     any_forward_ = true;
 }
 
-void Device::upload(const HostModel &m)
+void Device::bind(const ModelImage &img)
 {
-    const int d = hp_.n_embd, f = hp_.n_intermediate;
-    if (d % 64 || d > 1024 || f % 64 || (d / hp_.n_head != 32 && d / hp_.n_head != 64)) {
-        std::fprintf(stderr, "libbert: unsupported shape n_embd=%d n_intermediate=%d head_dim=%d "
-                             "(need n_embd %% 64 == 0, n_embd <= 1024, head_dim 32 or 64)\n",
-                     d, f, d / hp_.n_head);
-        return;
-    }
-    wfmt_ = hp_.ftype;
-    // f32 files run the f32 chain (f32.hip) on the file's own f32 rows; the other
-    // formats the lane-order layout of the MFMA f16 GEMMs
-    f32_ = wfmt_ == FMT_F32;
-    std::vector<Piece> pieces;
-    pieces.reserve(16 + 24 * (size_t)hp_.n_layer);
-    auto add = [&](Piece &&p) -> size_t { pieces.push_back(std::move(p)); return pieces.size() - 1; };
-    auto vec = [&](const HostTensor &t) -> size_t { Piece p; p.bytes = t.bytes; return add(std::move(p)); };
-    struct TabIdx { size_t q, d, m; };
-    auto table = [&](const HostTensor &t) -> TabIdx {
-        Piece q, dd, mm;
-        repack_table(t, q, dd, mm);
-        TabIdx r;
-        r.q = add(std::move(q)); r.d = add(std::move(dd)); r.m = add(std::move(mm));
-        return r;
+    wfmt_ = img.wfmt;
+    f32_ = img.f32;
+    auto P = [&](size_t i) -> void * {
+        return (i == ModelImage::kNone || img.len[i] == 0) ? nullptr : (void *)(arena_ + img.off[i]);
     };
-    struct LinIdx { size_t q, d, m; int N, K; };
-    auto linear = [&](std::vector<const HostTensor *> parts) -> LinIdx {
-        Piece q, dd, mm;
-        LinIdx r;
-        repack_linear(parts, wfmt_, q, dd, mm, r.N, r.K);
-        r.q = add(std::move(q)); r.d = add(std::move(dd)); r.m = add(std::move(mm));
-        return r;
-    };
-    const TabIdx tw = table(m.word), tt = table(m.ttype), tp = table(m.pos);
-    // f32 chain: the era's fp16 GELU and exp tables, built on the host (libm) as
-    // ggml built them, indexed on the device by the f16 bits of the input
-    size_t i_gelu = 0, i_exp = 0;
-    if (f32_) {
-        std::vector<uint16_t> tg, te;
-        era_tables(tg, te);
-        Piece pg, pe;
-        pg.bytes.assign((const uint8_t *)tg.data(), (const uint8_t *)(tg.data() + tg.size()));
-        pe.bytes.assign((const uint8_t *)te.data(), (const uint8_t *)(te.data() + te.size()));
-        i_gelu = add(std::move(pg));
-        i_exp = add(std::move(pe));
-    }
-    const size_t lnw = vec(m.ln_e_w), lnb = vec(m.ln_e_b);
-    auto fold = [&](std::vector<const HostTensor *> parts, std::vector<const HostTensor *> bias,
-                    const HostTensor &gamma, const HostTensor &beta, size_t &i1, size_t &i2) {
-        Piece c1, c2;
-        fold_ln(parts, bias, gamma, beta, c1, c2, wfmt_ == FMT_F32);
-        i1 = add(std::move(c1));
-        i2 = add(std::move(c2));
-    };
-    // f32 chain: the rows of the parts as f32 (concatenated along N)
-    auto rows32 = [&](std::vector<const HostTensor *> parts) -> size_t {
-        Piece p;
-        for (const HostTensor *t : parts) {
-            const size_t n0 = p.bytes.size();
-            p.bytes.resize(n0 + (size_t)t->ne1 * t->ne0 * 4);
-            for (int r = 0; r < t->ne1; ++r)
-                dequant_row(t->fmt, t->bytes.data() + fmt_row_bytes(t->fmt, t->ne0) * r,
-                            (float *)(p.bytes.data() + n0) + (size_t)r * t->ne0, t->ne0);
-        }
-        return add(std::move(p));
-    };
-    struct LIdx {
-        LinIdx qkv, o, up, down;
-        size_t bo, bdown, c1q, c2q, c1u, c2u, l1w, l1b, l2w, l2b;
-        size_t w32q, w32o, w32u, w32d, bq, bu;
-    };
-    std::vector<LIdx> li((size_t)hp_.n_layer);
-    for (int l = 0; l < hp_.n_layer; ++l) {
-        const HostLayer &L = m.layers[(size_t)l];
-        LIdx &x = li[(size_t)l];
-        if (f32_) {
-            x.w32q = rows32({&L.q_w, &L.k_w, &L.v_w}); x.w32o = rows32({&L.o_w});
-            x.w32u = rows32({&L.i_w}); x.w32d = rows32({&L.o2_w});
-            x.bq = rows32({&L.q_b, &L.k_b, &L.v_b}); x.bu = vec(L.i_b);
-            x.bo = vec(L.o_b); x.bdown = vec(L.o2_b);
-            x.l1w = vec(L.ln_att_w); x.l1b = vec(L.ln_att_b); x.l2w = vec(L.ln_out_w); x.l2b = vec(L.ln_out_b);
-            continue;
-        }
-        x.qkv = linear({&L.q_w, &L.k_w, &L.v_w});
-        x.o = linear({&L.o_w});
-        x.up = linear({&L.i_w});
-        x.down = linear({&L.o2_w});
-        // the LN in front of QKV: the previous layer's output LN, or the embedding LN
-        const HostTensor &gq = l ? m.layers[(size_t)l - 1].ln_out_w : m.ln_e_w;
-        const HostTensor &bq = l ? m.layers[(size_t)l - 1].ln_out_b : m.ln_e_b;
-        fold({&L.q_w, &L.k_w, &L.v_w}, {&L.q_b, &L.k_b, &L.v_b}, gq, bq, x.c1q, x.c2q);
-        fold({&L.i_w}, {&L.i_b}, L.ln_att_w, L.ln_att_b, x.c1u, x.c2u);
-        x.bo = vec(L.o_b); x.bdown = vec(L.o2_b);
-        x.l1w = vec(L.ln_att_w); x.l1b = vec(L.ln_att_b); x.l2w = vec(L.ln_out_w); x.l2b = vec(L.ln_out_b);
-    }
-    size_t total = 0;
-    for (Piece &p : pieces) { p.off = total; total += align_up(p.bytes.size(), 256); }
-    if (hipMalloc((void **)&arena_, total ? total : 256) != hipSuccess) {
-        std::fprintf(stderr, "libbert: hipMalloc of %zu bytes of weights failed on device %d\n", total, ordinal_);
-        arena_ = nullptr;
-        return;
-    }
-    arena_size_ = total;
-    for (Piece &p : pieces)
-        if (!p.bytes.empty() && hipMemcpy(arena_ + p.off, p.bytes.data(), p.bytes.size(), hipMemcpyHostToDevice) != hipSuccess) {
-            std::fprintf(stderr, "libbert: weight upload failed on device %d\n", ordinal_);
-            return;
-        }
-    auto P = [&](size_t i) -> void * { return pieces[i].bytes.empty() ? nullptr : (void *)(arena_ + pieces[i].off); };
-    auto mk_table = [&](const TabIdx &x, const HostTensor &t) {
+    auto mk_table = [&](const ModelImage::Tab &x) {
         DevTable r;
-        r.fmt = t.fmt; r.rows = t.ne1; r.cols = t.ne0;
+        r.fmt = x.fmt; r.rows = x.rows; r.cols = x.cols;
         r.qs = P(x.q); r.d = (const uint16_t *)P(x.d); r.m = (const uint16_t *)P(x.m);
         return r;
     };
     if (f32_) {
-        gelu_tab_ = (const uint16_t *)P(i_gelu);
-        exp_tab_ = (const uint16_t *)P(i_exp);
+        gelu_tab_ = (const uint16_t *)P(img.gelu);
+        exp_tab_ = (const uint16_t *)P(img.exp);
     }
-    word_ = mk_table(tw, m.word);
-    type_ = mk_table(tt, m.ttype);
-    pos_ = mk_table(tp, m.pos);
-    ln_e_w_ = (float *)P(lnw);
-    ln_e_b_ = (float *)P(lnb);
-    auto mk_lin = [&](const LinIdx &x) {
+    word_ = mk_table(img.word);
+    type_ = mk_table(img.type);
+    pos_ = mk_table(img.pos);
+    ln_e_w_ = (float *)P(img.lnw);
+    ln_e_b_ = (float *)P(img.lnb);
+    auto mk_lin = [&](const ModelImage::Lin &x) {
         DevWeight w;
         w.fmt = wfmt_ == FMT_F32 ? FMT_F16 : wfmt_; w.N = x.N; w.K = x.K;
         w.kx = wfmt_ == FMT_F32 ? x.K / 2 : 0;
         w.qs = P(x.q); w.d = (const uint16_t *)P(x.d); w.m = (const uint16_t *)P(x.m);
         return w;
     };
-    layers_.resize((size_t)hp_.n_layer);
+    layers_.assign((size_t)hp_.n_layer, DevLayer());
     for (int l = 0; l < hp_.n_layer; ++l) {
-        const LIdx &x = li[(size_t)l];
+        const ModelImage::Layer &x = img.layers[(size_t)l];
         DevLayer &D = layers_[(size_t)l];
         if (f32_) {
             D.w32_qkv = (const float *)P(x.w32q); D.w32_o = (const float *)P(x.w32o);
@@ -403,7 +481,6 @@ void Device::upload(const HostModel &m)
         D.c1_qkv = (float *)P(x.c1q); D.c2_qkv = (float *)P(x.c2q); D.c1_up = (float *)P(x.c1u); D.c2_up = (float *)P(x.c2u);
         D.ln1_w = (float *)P(x.l1w); D.ln1_b = (float *)P(x.l1b); D.ln2_w = (float *)P(x.l2w); D.ln2_b = (float *)P(x.l2b);
     }
-    ok_ = true;
 }
 
 bool Device::reserve(int64_t tokens, int64_t seqs, int max_len)
@@ -593,7 +670,7 @@ int Device::launch_all(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, in
         (void)hipStreamSynchronize(s);
         if (h) {
             bad = true;
-            std::fprintf(stderr, "libbert: BERT_CHECK_FINITE: %u non-finite values after %s (layer %d)\n", h, what, layer);
+            errorf("libbert: BERT_CHECK_FINITE: %u non-finite values after %s (layer %d)\n", h, what, layer);
         }
     };
 
@@ -684,7 +761,7 @@ int Device::launch_all(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, in
     if (cnt) (void)hipFree(cnt);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
-        std::fprintf(stderr, "libbert: kernel launch failed: %s\n", hipGetErrorString(e));
+        errorf("libbert: kernel launch failed: %s\n", hipGetErrorString(e));
         return -1;
     }
     return 0;
@@ -732,7 +809,7 @@ int Device::launch_all_f32(const int32_t *d_ids, const int32_t *d_cu, int n_seqs
     end(K_POOL_L2, s, ev, t * d * 4.0 + (double)n_seqs * d * 4.0);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
-        std::fprintf(stderr, "libbert: kernel launch failed: %s\n", hipGetErrorString(e));
+        errorf("libbert: kernel launch failed: %s\n", hipGetErrorString(e));
         return -1;
     }
     return 0;

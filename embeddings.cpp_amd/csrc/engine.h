@@ -62,10 +62,58 @@ private:
     hipError_t st_ = hipSuccess;
 };
 
+// A model's device image: every weight plane in its device layout (lane-order
+// linear weights, LN-fold constants, embedding-table planes, the f32 chain's
+// rows and tables), laid out at 256-B aligned offsets of one arena.  Built once
+// on the host by build_model_image and uploaded to every replica, so N replicas
+// cost one repack (reference: one read of the tensors, bert.cpp:650-766).
+struct ModelImage {
+    static constexpr size_t kNone = ~(size_t)0;
+    struct Tab { size_t q = kNone, d = kNone, m = kNone; int fmt = 0, rows = 0, cols = 0; };
+    struct Lin { size_t q = kNone, d = kNone, m = kNone; int N = 0, K = 0; };
+    struct Layer {
+        Lin qkv, o, up, down;
+        size_t bo = kNone, bdown = kNone, c1q = kNone, c2q = kNone, c1u = kNone, c2u = kNone;
+        size_t l1w = kNone, l1b = kNone, l2w = kNone, l2b = kNone;
+        size_t w32q = kNone, w32o = kNone, w32u = kNone, w32d = kNone, bq = kNone, bu = kNone;
+    };
+    HParams hp;
+    int wfmt = FMT_F16;
+    bool f32 = false;
+    Tab word, type, pos;
+    size_t gelu = kNone, exp = kNone, lnw = kNone, lnb = kNone;
+    std::vector<Layer> layers;
+    // piece i: bytes [off[i], off[i] + len[i]) of the image (len 0: absent plane)
+    std::vector<size_t> off, len;
+    size_t total = 0;
+    const uint8_t *bytes() const { return pinned_ ? pinned_ : host_.data(); }
+    bool pinned() const { return pinned_ != nullptr; }
+
+    ModelImage() = default;
+    ~ModelImage();
+    ModelImage(const ModelImage &) = delete;
+    ModelImage &operator=(const ModelImage &) = delete;
+
+private:
+    friend bool build_model_image(const HostModel &m, ModelImage &img, std::string &err, bool pin);
+    std::vector<uint8_t> host_;       // pageable image (when pinning failed or no device)
+    uint8_t *pinned_ = nullptr;       // page-locked image (hipHostMalloc): async uploads
+};
+
+// Host work of a load, once per context: checks the shape, repacks every plane
+// and concatenates them into the image (page-locked when `pin`).  False with a
+// message in err; never throws (a bad_alloc becomes false).
+bool build_model_image(const HostModel &m, ModelImage &img, std::string &err, bool pin);
+
 class Device {
 public:
-    Device(int ordinal, const HostModel &m);
+    // Creates the replica's stream and completion event, allocates the weight
+    // arena and issues the image upload on the replica's stream (async from a
+    // page-locked image).  Call finish_load() before the first use.  All HIP calls
+    // of a load are made by the loading thread (bert_load_from_file).
+    Device(int ordinal, const ModelImage &img);
     ~Device();
+    bool finish_load();   // waits for the upload; ok() from then on
     bool ok() const { return ok_; }
     int ordinal() const { return ordinal_; }
     hipStream_t stream() const { return stream_; }
@@ -134,8 +182,8 @@ private:
     int launch_all_f32(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, int max_len, int T, float *d_out,
                        hipStream_t s);
     void drop_graphs();
-    void upload(const HostModel &m);
-    void *arena_alloc(size_t bytes);
+    void bind(const ModelImage &img);   // device pointers of the image's planes
+    bool uploading_ = false;
     void begin(int cls, hipStream_t s, hipEvent_t &a);
     void end(int cls, hipStream_t s, hipEvent_t a, double work);
     hipEvent_t get_event();

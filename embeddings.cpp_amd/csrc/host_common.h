@@ -68,6 +68,15 @@ struct HostModel {
 // returns false with a message in err (the caller prints it to stderr).
 bool load_model_file(const char *path, HostModel &m, std::string &err, bool verbose);
 
+// Message sink (log.cpp): errorf prints to stderr, infof to stdout, trace nowhere
+// but the BERT_LOG file; all three append the line to BERT_LOG=<file> when set
+// (one unbuffered write per line).  fault_inject(stage): true when the test-only
+// BERT_FAULT_INJECT list names `stage`.
+void errorf(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
+void infof(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
+void trace(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
+bool fault_inject(const char *stage);
+
 // Dequantize one row of k elements into f32.
 void dequant_row(int fmt, const uint8_t *src, float *dst, int64_t k);
 // One row of k values in file format `fmt` (the quantizer's block rules).

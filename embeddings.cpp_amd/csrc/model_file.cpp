@@ -307,17 +307,17 @@ void quantize_row(int fmt, const float *x, uint8_t *dst, int64_t k)
 int quantize_file(const char *in, const char *out, int itype, bool verbose)
 {
     if (itype != FMT_Q4_0 && itype != FMT_Q4_1 && itype != FMT_Q8_0) {
-        std::fprintf(stderr, "bert_model_quantize: invalid quantization type %d\n", itype);
+        errorf("bert_model_quantize: invalid quantization type %d\n", itype);
         return 1;
     }
     File fi(in, "rb");
-    if (!fi.f) { std::fprintf(stderr, "bert_model_quantize: failed to open '%s' for reading\n", in); return 1; }
+    if (!fi.f) { errorf("bert_model_quantize: failed to open '%s' for reading\n", in); return 1; }
     File fo(out, "wb");
-    if (!fo.f) { std::fprintf(stderr, "bert_model_quantize: failed to open '%s' for writing\n", out); return 1; }
+    if (!fo.f) { errorf("bert_model_quantize: failed to open '%s' for writing\n", out); return 1; }
     uint32_t magic = 0;
     int32_t hp[7];
     if (!fi.read(&magic, 4) || magic != 0x67676d6cu || !fi.read(hp, sizeof(hp))) {
-        std::fprintf(stderr, "bert_model_quantize: invalid model file '%s' (bad magic)\n", in);
+        errorf("bert_model_quantize: invalid model file '%s' (bad magic)\n", in);
         return 1;
     }
     hp[6] = itype;
@@ -351,10 +351,10 @@ int quantize_file(const char *in, const char *out, int itype, bool verbose)
         org += (size_t)ne[0] * ne[1] * 4;
         if (q) {
             if (h3[2] != FMT_F32 && h3[2] != FMT_F16) {
-                std::fprintf(stderr, "bert_model_quantize: unsupported ftype %d for integer quantization\n", h3[2]);
+                errorf("bert_model_quantize: unsupported ftype %d for integer quantization\n", h3[2]);
                 return 1;
             }
-            if (ne[0] % QK) { std::fprintf(stderr, "bert_model_quantize: row of '%s' not a multiple of 32\n", name.c_str()); return 1; }
+            if (ne[0] % QK) { errorf("bert_model_quantize: row of '%s' not a multiple of 32\n", name.c_str()); return 1; }
             std::vector<float> row((size_t)ne[0]);
             std::vector<uint8_t> qrow(fmt_row_bytes(itype, ne[0]));
             const size_t rb = fmt_row_bytes(h3[2], ne[0]);

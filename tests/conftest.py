@@ -14,6 +14,31 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); calls the HIP path through the C ABI")
+    _route_library_log()
+
+
+def _route_library_log():
+    """BERT_LOG (csrc/log.cpp): libbert appends every error line (and the load path's
+    progress lines) to it with one unbuffered write each, so a native abort still
+    leaves its cause behind -- pytest's fd capture loses the test's stderr when the
+    process dies.  Here (pytest_configure, before any capture) fd 2 is the run's own
+    log (the driver's pytest.log); a duplicate of it is handed over as
+    fd:<n>:<dev>:<ino>, so the library's lines share its offset and land in order.
+    When fd 2 is not a regular file, a file under gpurun_out/ (merged back by gpurun)."""
+    if os.environ.get("BERT_LOG"):
+        return
+    try:
+        st = os.fstat(2)
+        import stat as _stat
+        if _stat.S_ISREG(st.st_mode):
+            fd = os.dup(2)
+            os.environ["BERT_LOG"] = f"fd:{fd}:{st.st_dev}:{st.st_ino}"
+            return
+    except OSError:
+        pass
+    out = os.path.join(ROOT, "gpurun_out")
+    os.makedirs(out, exist_ok=True)
+    os.environ["BERT_LOG"] = os.path.join(out, "libbert_tests.log")
 
 
 def _ensure(artifact, make_dir):

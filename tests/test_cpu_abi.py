@@ -273,3 +273,81 @@ def test_converter_cli_and_errors(lib, tmp_path):
     assert lib.bertx_convert_hf(bad.encode(), str(tmp_path / "x.bin").encode(), 0) != 0
     os.remove(os.path.join(bad, "model.safetensors"))
     assert lib.bertx_convert_hf(bad.encode(), str(tmp_path / "x.bin").encode(), 0) != 0
+
+
+_LOAD_PROBE = r"""
+import ctypes, sys
+L = ctypes.CDLL(sys.argv[1])
+L.bert_load_from_file.restype = ctypes.c_void_p
+L.bert_load_from_file.argtypes = [ctypes.c_char_p]
+ctx = L.bert_load_from_file(sys.argv[2].encode())
+print("CTX", "NULL" if not ctx else "OK", flush=True)
+"""
+
+
+def _load_in_child(tmp_path, model, env_extra):
+    """bert_load_from_file in a fresh process, so an abort shows as its exit status
+    instead of killing the test run; returns (returncode, stdout, BERT_LOG text)."""
+    log = tmp_path / "libbert.log"
+    env = dict(os.environ)
+    env.pop("BERT_HOST_ONLY", None)
+    env.update(env_extra)
+    env["BERT_LOG"] = str(log)
+    p = subprocess.run([os.sys.executable, "-c", _LOAD_PROBE, os.path.join(ROOT, "build", "libbert.so"), model],
+                       capture_output=True, text=True, env=env, timeout=120)
+    return p.returncode, p.stdout + p.stderr, log.read_text() if log.exists() else ""
+
+
+@pytest.mark.parametrize("stage", ["load", "image"])
+def test_injected_load_failure_returns_null(lib, tmp_path, stage):
+    """Every failure of the load path is a NULL context plus a message, never an
+    abort (reference loader: bert.cpp:423-443, 684-750 print and return nullptr).
+    BERT_FAULT_INJECT makes a load stage throw: `load` at the entry, `image` inside the
+    host repack (a bad_alloc, as a host out-of-memory would).  The process must exit
+    normally with a NULL context, and the BERT_LOG sink must hold the cause."""
+    rc, out, log = _load_in_child(tmp_path, os.path.join(GOLDEN, "tiny32", "ggml-model-f16.bin"),
+                                  {"BERT_FAULT_INJECT": stage})
+    assert rc == 0, (rc, out)
+    assert "CTX NULL" in out, out
+    want = "load failed: BERT_FAULT_INJECT=load" if stage == "load" else "out of host memory building the device image"
+    assert want in log, log
+    assert want in out   # ... and the same line on stderr
+
+
+@pytest.mark.skipif(HAS_GPU_NODE, reason="checks the no-device failure path")
+def test_bert_log_sink_records_errors(lib, tmp_path):
+    """BERT_LOG=<file> receives every libbert error line (and the load path's
+    progress lines) with the pid, unbuffered: here the no-device refusal."""
+    rc, out, log = _load_in_child(tmp_path, os.path.join(GOLDEN, "tiny32", "ggml-model-f32.bin"), {})
+    assert rc == 0 and "CTX NULL" in out, (rc, out)
+    assert "no HIP (gfx950) device available" in log, log
+    assert "building the device image" in log and f"[" in log.splitlines()[0]
+
+
+def test_bert_log_fd_form_checks_identity(lib, tmp_path):
+    """BERT_LOG=fd:<n>:<dev>:<ino> (tests/conftest.py hands pytest's stderr over this
+    way) writes to descriptor n only while it is that file: a child process in which
+    n is another file writes nothing there."""
+    target = tmp_path / "target.log"
+    other = tmp_path / "other.log"
+    code = r"""
+import ctypes, os, sys
+fd = os.open(sys.argv[2], os.O_WRONLY | os.O_CREAT | os.O_APPEND)
+os.environ["BERT_LOG"] = sys.argv[3].replace("N", str(fd))
+L = ctypes.CDLL(sys.argv[1])
+L.bert_load_from_file.restype = ctypes.c_void_p
+L.bert_load_from_file(b"/nonexistent/model.bin")
+"""
+    st = os.stat(target.parent)   # a different file's identity: must not be written
+    so = os.path.join(ROOT, "build", "libbert.so")
+    env = dict(os.environ)
+    env.pop("BERT_LOG", None)
+    subprocess.run([os.sys.executable, "-c", code, so, str(other), f"fd:N:{st.st_dev}:{st.st_ino}"],
+                   env=env, check=True, capture_output=True, timeout=120)
+    assert other.read_text() == ""
+    # the matching identity: written
+    target.write_text("")
+    st = os.stat(target)
+    subprocess.run([os.sys.executable, "-c", code, so, str(target), f"fd:N:{st.st_dev}:{st.st_ino}"],
+                   env=env, check=True, capture_output=True, timeout=120)
+    assert "bert_load_from_file" in target.read_text()

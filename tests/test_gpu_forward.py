@@ -476,3 +476,41 @@ def test_routing_small_calls_to_distinct_replicas(quant_models, monkeypatch):
     assert [b - a for a, b in zip(c2, c3)] == [1, 1, 1, 1], (c2, c3)
     assert [p[1] for p in m4.device_last_call()] == [16] * 4
     assert np.array_equal(out, ref)
+
+
+@pytest.mark.parametrize("stage", ["replica1", "worker"])
+def test_injected_replica_failure_returns_null(quant_models, tmp_path, stage):
+    """Round 5's driver run aborted inside bert_load_from_file with 4 replicas
+    (DESIGN §11).  The load now runs every HIP call on the loading thread and turns
+    every failure into a NULL context: BERT_FAULT_INJECT throws while the second
+    replica is being made (`replica1`, after the first one's upload was issued) or
+    while the replica workers start (`worker`, a std::system_error as from
+    std::thread).  In a child process (an abort shows as its exit status): NULL,
+    exit 0, the cause in BERT_LOG, and a normal 4-replica load in the same process
+    afterwards works and runs a forward (the failed replicas were released)."""
+    import subprocess
+    import sys
+    code = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+import numpy as np, os, bertpy
+L = bertpy.load_lib()
+ctx = L.bert_load_from_file(sys.argv[2].encode())
+print("FIRST", "NULL" if not ctx else "OK", flush=True)
+os.environ.pop("BERT_FAULT_INJECT")   # read per load stage: the next load is clean
+m = bertpy.BertModel(sys.argv[2])
+print("SECOND", m.lib.bertx_num_devices(m.ctx), flush=True)
+e = m.forward_batch([np.arange(5, 40, dtype=np.int32)])
+print("FWD", bool(np.isfinite(e).all()), flush=True)
+"""
+    log = tmp_path / "libbert.log"
+    env = dict(os.environ, BERT_DEVICES="0,0,0,0", BERT_FAULT_INJECT=stage, BERT_LOG=str(log))
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-c", code, os.path.join(root, "embeddings.cpp_amd"),
+                        quant_models[("tiny64", "q4_0")]], capture_output=True, text=True, env=env, timeout=120)
+    out = p.stdout + p.stderr
+    assert p.returncode == 0, out
+    assert "FIRST NULL" in out, out
+    text = log.read_text()
+    assert f"BERT_FAULT_INJECT={stage}" in text, text
+    assert "SECOND 4" in out and "FWD True" in out, out
