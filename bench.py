@@ -72,12 +72,10 @@ def launch_ranks(a):
     process has imported torch or touched a GPU (never a re-exec of a process that
     has initialised the GPU) -- and exit with its status.  Rank 0 prints the JSON
     line to the inherited stdout."""
-    import socket
-    with socket.socket() as so:
-        so.bind(("127.0.0.1", 0))
-        port = so.getsockname()[1]
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
-           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    # --standalone: the launcher binds its own free rendezvous port (no window between
+    # choosing a port here and binding it there, ADVICE r5), on 127.0.0.1
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
+           f"--nproc-per-node={a.gpus}", os.path.abspath(__file__)] + sys.argv[1:]
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     return subprocess.run(cmd, env=env).returncode
 
@@ -411,6 +409,17 @@ def probes(lib, bertpy, torch, a, dev, stream, q4_path):
     return out
 
 
+def all_ranks_ok(ok, dist, red_dev):
+    """True on every rank iff `ok` is True on every rank (a MIN all-reduce; no
+    collective without torch.distributed)."""
+    if dist is None:
+        return ok
+    import torch
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=red_dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
 def library_path(model, ids_list, steps, dist, red_dev):
     """The reference Python client's path (examples/sample_dylib.py -> bert_forward_batch):
     host int32 token arrays in, host float32 rows out -- staging copy, H2D, forward,
@@ -432,22 +441,31 @@ def encode_path(lib, model, ids_list, steps, dist, red_dev, ref):
     stage alone (bertx_tokenize_batch, bert_encode_batch's first stage) to report
     its share of the call."""
     import numpy as np
-    texts = [" ".join("w%d" % (int(t) - 104) for t in ids[1:-1]).encode() for ids in ids_list]
-    toks, n = model.tokenize(texts[0])
-    if n != len(ids_list[0]) or toks != [int(x) for x in ids_list[0]]:
-        raise RuntimeError("encode texts do not tokenize to the bench ids")
-    share = len(os.sched_getaffinity(0))
-    n_thr = max(1, min(share, int(os.environ.get("OMP_NUM_THREADS", share))))
-    B, d = len(texts), model.n_embd
-    out = np.zeros((B, d), np.float32)
-    rows = (out.ctypes.data + out.strides[0] * np.arange(B, dtype=np.uintp)).astype(np.uintp)
-    rows_p = rows.ctypes.data_as(ctypes.POINTER(ctypes.POINTER(ctypes.c_float)))
-    carr = (ctypes.c_char_p * B)(*texts)
+    # rank-local preparation, then every rank agrees before the collectives of the
+    # timed region: a rank that failed here (e.g. a tokenize mismatch) must not leave
+    # the others waiting in its barrier (ADVICE r5)
+    err = None
+    try:
+        texts = [" ".join("w%d" % (int(t) - 104) for t in ids[1:-1]).encode() for ids in ids_list]
+        toks, n = model.tokenize(texts[0])
+        if n != len(ids_list[0]) or toks != [int(x) for x in ids_list[0]]:
+            raise RuntimeError("encode texts do not tokenize to the bench ids")
+        share = len(os.sched_getaffinity(0))
+        n_thr = max(1, min(share, int(os.environ.get("OMP_NUM_THREADS", share))))
+        B, d = len(texts), model.n_embd
+        out = np.zeros((B, d), np.float32)
+        rows = (out.ctypes.data + out.strides[0] * np.arange(B, dtype=np.uintp)).astype(np.uintp)
+        rows_p = rows.ctypes.data_as(ctypes.POINTER(ctypes.POINTER(ctypes.c_float)))
+        carr = (ctypes.c_char_p * B)(*texts)
 
-    def call():
-        lib.bert_encode_batch(model.ctx, n_thr, B, B, carr, rows_p)
-    for _ in range(2):
-        call()
+        def call():
+            lib.bert_encode_batch(model.ctx, n_thr, B, B, carr, rows_p)
+        for _ in range(2):
+            call()
+    except Exception as ex:   # noqa: BLE001 -- agreed on below, then reported
+        err = ex
+    if not all_ranks_ok(err is None, dist, red_dev):
+        raise RuntimeError(f"encode leg skipped on every rank ({err or 'another rank failed its preparation'})")
     same = bool(ref is not None and np.array_equal(out, ref))
     cos = float(np.min(np.sum(out * ref, axis=1))) if ref is not None else None
     el = timed_steps(call, steps, lambda: None, dist, red_dev)

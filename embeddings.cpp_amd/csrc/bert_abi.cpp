@@ -98,13 +98,16 @@ namespace {
 constexpr int64_t kChunkTokens = 1 << 17;   // tokens per device forward (workspace bound)
 constexpr int kChunkSeqs = 4096;            // sentences per device forward (pool / output staging bound)
 // A call is split only over replicas that are idle (no routed work in flight), and
-// only while each share keeps at least kMinShareTokens.  Measured per-share latency
-// on one replica (scripts/share_curve.py, profiles/r05_share_curve.jsonl: bge-base
-// q4_0, 128-token sentences through bert_forward_batch): the cost per token is 4.7x
-// the large-batch asymptote at 128 tokens, 1.8x at 4,096, 1.26x at 8,192 and 1.07x
-// at 16,384 -- below 8,192 tokens a forward is launch- and latency-bound, so a
-// smaller share buys little latency and costs its replica a whole forward.  A call
-// that finds no idle replica goes whole to the least-loaded one, so concurrent
+// only while each share keeps at least kMinShareTokens.  The choice, from the
+// measured per-share latency on one replica (scripts/share_curve.py,
+// profiles/r05_share_curve.jsonl: bge-base q4_0, 128-token sentences through
+// bert_forward_batch): the cost per token is 4.7x the large-batch asymptote at 128
+// tokens, 1.8x at 4,096, 1.26x at 8,192 and 1.07x at 16,384.  The curve's own knee
+// criterion (within 1.25x of the asymptote) gives 16,384; 8,192 is the smallest
+// share for which a 2-way split still pays: a 16,384-token call takes 3.63 ms on one
+// replica and 2.14 ms as two 8,192-token shares, while at 4,096 tokens per share
+// (1.52 ms) the two half-size forwards buy 0.6 ms for a whole second replica.  A
+// call that finds no idle replica goes whole to the least-loaded one, so concurrent
 // callers (the server's batchers) land on different replicas instead of all
 // splitting over all of them in lockstep.
 constexpr int64_t kMinShareTokens = 8192;
@@ -387,12 +390,12 @@ static bert_ctx *load_context(const char *fname)
     }
     const std::vector<int> devs = parse_device_list(emb::hip_device_count());
     // the host half of the load, once for all replicas: repack into one image
-    emb::trace("bert_load_from_file: building the device image\n");
     if (!emb::build_model_image(m, img, err, !devs.empty())) {
         emb::errorf("bert_load_from_file: %s\n", err.c_str());
         return nullptr;
     }
-    emb::trace("bert_load_from_file: image %zu bytes (%s)\n", img.total, img.pinned() ? "page-locked" : "pageable");
+    emb::trace("bert_load_from_file: '%s': image %zu bytes (%s), %zu replica(s)\n", fname, img.total,
+               img.pinned() ? "page-locked" : "pageable", devs.size());
     { emb::HostModel none; std::swap(m.layers, none.layers); }   // the file tensors are no longer needed
     if (devs.empty()) {
         emb::errorf("bert_load_from_file: no HIP (gfx950) device available -- libbert.so has no CPU "
@@ -400,7 +403,7 @@ static bert_ctx *load_context(const char *fname)
         return nullptr;
     }
     for (size_t i = 0; i < devs.size(); ++i) {
-        emb::trace("bert_load_from_file: replica %zu on device %d: create + upload\n", i, devs[i]);
+        if (devs.size() > 1) emb::trace("bert_load_from_file: replica %zu on device %d: create + upload\n", i, devs[i]);
         if (i == 1 && emb::fault_inject("replica1")) throw std::runtime_error("BERT_FAULT_INJECT=replica1");
         ctx->devices.emplace_back(new Device(devs[i], img));
     }

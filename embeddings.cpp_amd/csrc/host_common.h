@@ -68,9 +68,9 @@ struct HostModel {
 // returns false with a message in err (the caller prints it to stderr).
 bool load_model_file(const char *path, HostModel &m, std::string &err, bool verbose);
 
-// Message sink (log.cpp): errorf prints to stderr, infof to stdout, trace nowhere
-// but the BERT_LOG file; all three append the line to BERT_LOG=<file> when set
-// (one unbuffered write per line).  fault_inject(stage): true when the test-only
+// Message sink (log.cpp): errorf prints to stderr and appends the line to
+// BERT_LOG=<file> when set (one unbuffered write per line); trace writes to the
+// BERT_LOG file only (the load path's stages); infof prints to stdout only.  fault_inject(stage): true when the test-only
 // BERT_FAULT_INJECT list names `stage`.
 void errorf(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
 void infof(const char *fmt, ...) __attribute__((format(printf, 1, 2)));

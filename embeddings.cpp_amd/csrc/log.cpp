@@ -3,7 +3,8 @@
 // and -- when BERT_LOG=<file> is set -- is also appended to that file with one
 // unbuffered write(2) per line, so the cause of a failure survives a process
 // that dies right after it (pytest's fd capture loses stderr on an abort).
-// Progress lines of the load path go to the file only (emb::trace).
+// Stage lines of the load path go to the file only (emb::trace); informational
+// lines (emb::infof) to stdout only.
 #include "host_common.h"
 
 #include <fcntl.h>
@@ -75,8 +76,9 @@ void infof(const char *fmt, ...)
 {
     va_list ap;
     va_start(ap, fmt);
-    emit(stdout, fmt, ap);
+    std::vfprintf(stdout, fmt, ap);   // progress for the caller's stdout only (not BERT_LOG)
     va_end(ap);
+    std::fflush(stdout);
 }
 
 void trace(const char *fmt, ...)

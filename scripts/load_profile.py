@@ -51,10 +51,13 @@ def main():
     ap.add_argument("--repeat", type=int, default=2)
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
-    import bertpy
     tmp = tempfile.mkdtemp(prefix="loadprof_")
     path = os.path.join(tmp, f"{a.arch}-{a.ftype}.bin")
-    bertpy.synthetic_model(path, a.arch, a.ftype, seed=1234)
+    # the model is written by a child too: this process stays small, so the load
+    # children (whose peak RSS starts from the parent's at fork) measure the load
+    subprocess.run([sys.executable, "-c", "import sys; sys.path.insert(0, sys.argv[1]); import bertpy; "
+                    "bertpy.synthetic_model(sys.argv[2], sys.argv[3], sys.argv[4], seed=1234)",
+                    os.path.join(ROOT, "embeddings.cpp_amd"), path, a.arch, a.ftype], check=True)
     size = os.path.getsize(path)
     rows = []
     for rep in range(a.repeat):

@@ -47,8 +47,10 @@ def lib():
         L.oracle_exp.argtypes = [ctypes.c_float]
         L.oracle_quantize_row.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         L.oracle_dequantize_row.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
-        L.oracle_set_activation_f32.argtypes = [ctypes.c_int]
-        L.oracle_get_activation_f32.restype = ctypes.c_int
+        for fn in (L.oracle_forward_batch_ex, L.oracle_forward_fake_batch_ex):
+            fn.restype = ctypes.c_int
+            fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int32),
+                           ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_float)]
         _lib = L
     return _lib
 
@@ -93,29 +95,24 @@ class Oracle:
 
     def _fwd(self, fn, ids_list, n_threads, activations="q8"):
         """activations "q8": the reference's arithmetic (q4/q8 weights x q8_0 / q8_1
-        re-quantized activations); "f32": the diagnostic switch (the same weights x the
-        f32 activations, oracle_set_activation_f32) -- only to measure how far the
-        reference's activation rounding moves an embedding, never as the parity bar."""
+        re-quantized activations); "f32": the diagnostic mode (the same weights x the
+        f32 activations, a per-call argument of oracle_forward_batch_ex) -- only to
+        measure how far the reference's activation rounding moves an embedding, never
+        as the parity bar."""
         assert activations in ("q8", "f32")
-        if activations == "f32":
-            lib().oracle_set_activation_f32(1)
-            try:
-                return self._fwd(fn, ids_list, n_threads)
-            finally:
-                lib().oracle_set_activation_f32(0)
         flat = np.ascontiguousarray(np.concatenate([np.asarray(x, np.int32) for x in ids_list]))
         lens = np.asarray([len(x) for x in ids_list], np.int32)
         out = np.zeros((len(ids_list), self.n_embd), np.float32)
-        rc = fn(self.h, n_threads, len(ids_list), _i32(flat), _i32(lens), _f32(out))
+        rc = fn(self.h, n_threads, 1 if activations == "f32" else 0, len(ids_list), _i32(flat), _i32(lens), _f32(out))
         if rc != 0:
             return None
         return out
 
     def forward_batch(self, ids_list, n_threads=8, activations="q8"):
-        return self._fwd(lib().oracle_forward_batch, ids_list, n_threads, activations)
+        return self._fwd(lib().oracle_forward_batch_ex, ids_list, n_threads, activations)
 
     def forward_fake_batch(self, ids_list, n_threads=8, activations="q8"):
-        return self._fwd(lib().oracle_forward_fake_batch, ids_list, n_threads, activations)
+        return self._fwd(lib().oracle_forward_fake_batch_ex, ids_list, n_threads, activations)
 
     def encode_batch(self, texts, n_batch_size, n_threads=8):
         n = len(texts)

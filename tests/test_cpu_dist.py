@@ -137,3 +137,34 @@ def test_bench_refuses_world_mismatch():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-step"], cwd="/tmp",
                        env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=120)
     assert r.returncode != 0 and b"WORLD_SIZE 1" in r.stderr
+
+
+def _agree_worker(rank, world, port, q):
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    both = bench.all_ranks_ok(True, dist, "cpu")
+    one_fails = bench.all_ranks_ok(rank != 1, dist, "cpu")   # rank 1's preparation failed
+    q.put((rank, both, one_fails))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_optional_leg_agreement_gloo():
+    """an optional bench leg (the encode path) prepares rank-locally, then
+    every rank agrees (bench.all_ranks_ok, a MIN all-reduce) before the leg's
+    collectives, so one rank's failure skips the leg everywhere instead of leaving
+    the other ranks blocked in its barrier."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_agree_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == [(0, True, False), (1, True, False)]

@@ -220,13 +220,14 @@ def test_oracle_encode_batch(oracle):
         assert float(np.dot(single, e)) > 1 - 1e-5
 
 
-def test_activation_f32_switch(oracle, quant_models):
-    """The diagnostic switch (oracle_set_activation_f32): quantized
-    weights times f32 activations instead of the reference's q8 re-quantized ones.
-    It changes only the quantized-weight matmuls (f16 / f32 files bitwise
-    unchanged), moves a tiny q4_0 model by a little (the q8 rounding), brings it
-    closer to the f32-weight forward of the same model, and is restored after the
-    call."""
+def test_activation_f32_mode(oracle, quant_models):
+    """The diagnostic mode (oracle_forward_batch_ex's act_f32 argument):
+    quantized weights times f32 activations instead of the reference's q8
+    re-quantized ones.  It changes only the quantized-weight matmuls (f16 / f32 files
+    bitwise unchanged), moves a tiny q4_0 model by a little (the q8 rounding), brings
+    it closer to the f32-weight forward of the same model, and -- a per-call argument,
+    not process state -- leaves every other call in the reference's arithmetic, also
+    one running concurrently on another thread."""
     z = np.load(f"{GOLDEN}/tiny64/forward_f32.npz")
     seqs = np.split(z["ids"], np.cumsum(z["lens"])[:-1])[:6]
     ref = oracle.Oracle(quant_models[("tiny64", "f32")]).forward_batch(seqs)
@@ -236,13 +237,28 @@ def test_activation_f32_switch(oracle, quant_models):
     o = oracle.Oracle(quant_models[("tiny64", "q8_0")])
     q8 = o.forward_batch(seqs)
     f32 = o.forward_batch(seqs, activations="f32")
-    assert oracle.lib().oracle_get_activation_f32() == 0
     assert not np.array_equal(q8, f32)
     c_q8 = np.sum(q8 * ref, axis=1)
     c_f32 = np.sum(f32 * ref, axis=1)
     assert np.all(np.sum(q8 * f32, axis=1) > 1 - 1e-3)
     assert np.mean(1 - c_f32) <= np.mean(1 - c_q8)
     assert np.array_equal(o.forward_batch(seqs), q8)
+    # concurrent callers (ctypes releases the GIL): each keeps its own arithmetic, and
+    # the lazily made f32 weight cache is built once under a lock
+    import threading
+    o2 = oracle.Oracle(quant_models[("tiny64", "q4_0")])
+    res = {}
+
+    def run(k, act):
+        res[k] = o2.forward_batch(seqs, n_threads=2, activations=act)
+    th = [threading.Thread(target=run, args=(k, "f32" if k % 2 else "q8")) for k in range(6)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    want_q8, want_f32 = o2.forward_batch(seqs), o2.forward_batch(seqs, activations="f32")
+    for k in range(6):
+        assert np.array_equal(res[k], want_f32 if k % 2 else want_q8), k
 
 
 def _model_tensors(oracle, path):
