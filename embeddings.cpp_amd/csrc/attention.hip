@@ -1,5 +1,6 @@
 // Flash-style self-attention for gfx950 (reference bert.cpp:1018-1036).
 #include "device_common.h"
+#include "diag_att_stamps.h"
 #include "kernels.h"
 
 #include <cmath>
@@ -376,21 +377,6 @@ __device__ __forceinline__ void wait_all_vm()
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-#ifdef ATT_STAMPS
-// Diagnostic build only (make EXTRA=-DATT_STAMPS BUILD=...): per wave and item
-// (at most 4 items per workgroup) s_memtime at the item's start, after block 0,
-// at B1's arrival, after B1, at the block loop's end, after S, after the stores,
-// and the wave's HW_ID (scripts/att_stamps.py)
-__device__ unsigned long long g_att_stamps[1 << 17];
-#define ASTAMP(k, v) do { if (lane == 0 && nit < 4) g_att_stamps[(((size_t)blockIdx.x * 16 + w) * 4 + nit) * 8 + (k)] = (v); } while (0)
-extern "C" __attribute__((visibility("default"))) int bertx_att_stamps(unsigned long long *host, size_t n)
-{
-    if (n > (1u << 17)) n = 1u << 17;
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_att_stamps), n * 8) == hipSuccess ? 0 : -1;
-}
-#else
-#define ASTAMP(k, v) do { } while (0)
-#endif
 
 __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restrict__ qkv,
                                                               const int32_t *__restrict__ cu, int d, int nh,
@@ -580,9 +566,7 @@ __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restr
     __syncthreads();
     const h16 s16 = (h16)sl2;
     const h16x8 sc = {s16, s16, s16, s16, s16, s16, s16, s16};
-#ifdef ATT_STAMPS
-    int nit = 0;
-#endif
+    ASTAMP_ITEMS(nit);   // (stamps builds only, diag_att_stamps.h)
     for (;;) {
         ASTAMP(0, __builtin_amdgcn_s_memtime());
         const int nx_i = cur_i + (int)gridDim.x;
@@ -700,10 +684,7 @@ __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restr
         __syncthreads();                                  // S: region B is free
         if (active) store_rows();
         ASTAMP(6, __builtin_amdgcn_s_memtime());
-#ifdef ATT_STAMPS
-        ASTAMP(7, (unsigned long long)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11)));
-        ++nit;
-#endif
+        ASTAMP_ITEM_END(nit);
         if (!more) break;
         cur = nx;
         cur_i = nx_i;

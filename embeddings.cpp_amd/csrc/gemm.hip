@@ -25,6 +25,7 @@
 // (16-B loads of bias / residual / LN parameters and one 16-B store); the
 // LayerNorm bookkeeping of kernels.h LnFold runs there.
 #include "device_common.h"
+#include "diag_gemm_stamps.h"
 #include "host_common.h"
 #include "kernels.h"
 #include "zregs.h"
@@ -38,15 +39,6 @@
 
 namespace emb {
 
-#ifdef GEMM_STAMPS
-// Diagnostic build only (make EXTRA=-DGEMM_STAMPS BUILD=...): per wave-tile
-// s_memtime at start / after the prologue / after the K loop / after the
-// epilogue, HW_ID, XCC_ID and the tile index (scripts/gemm_stamps.py)
-__device__ unsigned long long g_gemm_stamps[1 << 18];
-#define ZSTAMP(i, v) do { if ((threadIdx.x & 63) == 0) g_gemm_stamps[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + (i)] = (v); } while (0)
-#else
-#define ZSTAMP(i, v) do { } while (0)
-#endif
 
 namespace {
 
@@ -428,11 +420,9 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     const int sw = (fr >> 1) & 7;               // mt is a multiple of 32: the row swizzle is fr's
     const int rbase = PRIV ? fr << 7 : (mt + fr) << 7;
     int st = 0;
-#ifdef GEMM_STAMPS
-    // K-loop split (diagnostic): cycles in the load wait in front of each K-step's
-    // MFMAs, and in the wait + barrier behind them (slots 6, 7)
-    unsigned long long zw_front = 0, zw_back = 0;
-#endif
+    // K-loop split (stamps builds only, diag_gemm_stamps.h): cycles in the load wait
+    // in front of each K-step's MFMAs, and in the wait + barrier behind them
+    ZClock zc;
     // One K-step with CUR's weights: issue X(ks + NS - 1) into the stage freed by
     // the previous step and W(ks + WR - 1) into the ring's free register set,
     // then the derived vmcnt (z_waits: what is provably still in flight; a
@@ -481,42 +471,30 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
                 wload_or_tail(nxt, kw, tail);
                 wait_vmcnt<ZW.front>();
             } else if constexpr (NS == 2) {
-#ifdef GEMM_STAMPS
-                // (NS 2: slot 6 holds the cycles of the X pieces' issue instead of the front wait)
-                const unsigned long long zd = __builtin_amdgcn_s_memtime();
-#endif
+                // (NS 2: the front slot holds the cycles of the X pieces' issue instead of the wait)
+                zc.mark();
                 issue_x(kx, sx);
                 asm volatile("" ::: "memory");
-#ifdef GEMM_STAMPS
-                zw_front += __builtin_amdgcn_s_memtime() - zd;
-#endif
+                zc.add_front();
                 wload_or_tail(nxt, kw, tail);
                 wait_vmcnt<ZW.front>();
             } else {
                 wload_or_tail(nxt, kw, tail);
                 asm volatile("" ::: "memory");
                 issue_x(kx, sx);
-#ifdef GEMM_STAMPS
-                const unsigned long long za = __builtin_amdgcn_s_memtime();
-#endif
+                zc.mark();
                 wait_vmcnt<ZW.front>();
-#ifdef GEMM_STAMPS
-                zw_front += __builtin_amdgcn_s_memtime() - za;
-#endif
+                zc.add_front();
             }
             cur.pin_all();
             const uint32_t xs = lds_u32(smem + st * XB + rbase);
             h16x8 bq[PF + 1];
             zmma_items<NJ, FA, PF, false, false>(cur, xs + ((g ^ sw) << 4), xs + (((4 + g) ^ sw) << 4), acc, hook, bq,
                                                  std::make_integer_sequence<int, 2 * NJ>{});
-#ifdef GEMM_STAMPS
-            const unsigned long long zb = __builtin_amdgcn_s_memtime();
-#endif
+            zc.mark();
             wait_vmcnt<ZW.back>();
             lds_barrier();
-#ifdef GEMM_STAMPS
-            zw_back += __builtin_amdgcn_s_memtime() - zb;
-#endif
+            zc.add_back();
         }
         st = st == NS - 1 ? 0 : st + 1;
     };
@@ -591,12 +569,7 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
         lds_barrier();
     }
     ZSTAMP(2, __builtin_amdgcn_s_memtime());
-#ifdef GEMM_STAMPS
-    ZSTAMP(4, __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11)));
-    ZSTAMP(5, __builtin_amdgcn_s_getreg((20) | (0 << 6) | (31 << 11)));
-    ZSTAMP(6, zw_front);
-    ZSTAMP(7, zw_back);
-#endif
+    ZSTAMP_KSPLIT(zc);
 
     // ---- epilogue ----
     // acc[2 fa + a][j] lane (g, fr): token m0 + 16j + fr, features nw + 32fa + 16a + 4g + 0..3.
@@ -899,14 +872,6 @@ int device_cu_count()
     if (dev < 64) cache[dev].store(n, std::memory_order_relaxed);
     return n;
 }
-
-#ifdef GEMM_STAMPS
-extern "C" __attribute__((visibility("default"))) int bertx_gemm_stamps(unsigned long long *host, size_t n)
-{
-    if (n > (1u << 18)) n = 1u << 18;
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gemm_stamps), n * 8) == hipSuccess ? 0 : -1;
-}
-#endif
 
 int launch_gemm(const DevWeight &W, const uint16_t *X, int32_t M, const float *bias, int32_t epi, const void *res,
                 void *out, hipStream_t s, const LnFold &ln)
