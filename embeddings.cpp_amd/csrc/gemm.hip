@@ -287,6 +287,8 @@ __device__ __forceinline__ void gemmz_body(char *__restrict__ smem, const int b,
     // XCD-aware bijective remap: consecutive tiles (same token panel) land on one
     // XCD's L2 (workgroups are dealt to the 8 XCDs round-robin)
     const int xcd = b & 7, qq = nTiles >> 3, rr = nTiles & 7;
+    // (round 6 measured panel-group and snake orders of the tiles inside an XCD's
+    // share: within noise, and without the remap -13 %; profiles/r06_gemm_raster_ab.log)
     const int t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
     const int m0 = (t / nN) * BM, n0 = (t % nN) * BN;
     const int K = W.K, N = W.N, KS = K / ZK;
@@ -747,6 +749,7 @@ void dispatch_z(const DevWeight &W, const h16 *x, int M, const float *bias, int 
     // measured 1-2 us slower so, profiles/r02_gemm_persist_ab.log).  Whole
     // column tiles only.  BERT_GEMM_PERSIST = k forces k per CU, 0 = off.
     static const int persist_env = [] { const char *e = std::getenv("BERT_GEMM_PERSIST"); return e ? std::atoi(e) : -1; }();
+
     const int cus = device_cu_count();
     const int persist = persist_env >= 0 ? persist_env : (nTiles <= 2 * OCC * cus ? OCC : 0);
     int grid = nTiles;
