@@ -691,9 +691,163 @@ __global__ __launch_bounds__(1024) void attention_lds3_kernel(const h16 *__restr
     }
 }
 
-
+// ---------------------------------------------------------------------------
+// Short sentences (max_len <= 64, the serving shape: examples/server.cpp:114 ->
+// one text per bert_encode): one 2-wave workgroup per (sentence, head), the
+// item's one 64-key block.  attention_lds3 runs such an item on 16 waves of which
+// one or two have queries, through its region DMA and its B1 and S barriers;
+// here the K/V rows are plain 16-B loads into the same swizzled LDS image and
+// the block is lds3's block 0 instruction for instruction (the same MFMA chains
+// in the same order, the f16 row-max offset, the exp2 sum, P.V, 1 / l), so a
+// sentence gets the same bits from either kernel (batch-composition invariance:
+// a short sentence alone takes this kernel, inside a longer batch lds3).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(128) void attention_short_kernel(const h16 *__restrict__ qkv,
+                                                              const int32_t *__restrict__ cu, int d, int nh,
+                                                              float sl2, h16 *__restrict__ out)
+{
+    constexpr int DH = 64, RB = DH * 2, NK = 64, VB = NK * RB;
+    __shared__ __attribute__((aligned(16))) char smem[2 * NK * RB];
+    const int it = blockIdx.x, b = it / nh, h = it - b * nh;
+    const int start = cu[b], len = cu[b + 1] - start;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int hi = lane >> 5, lq = lane & 31;
+    const int ld = 3 * d;
+    if (len <= 0) return;                                 // workgroup-uniform
+    // the wave's Q rows first: their loads fly with the K / V loads below
+    h16x8 qf[DH / 16];
+    {
+        const h16 *qrow = qkv + (size_t)(start + min(32 * w + lq, len - 1)) * ld + h * DH;
+#pragma unroll
+        for (int st = 0; st < DH / 16; ++st) qf[st] = *(const h16x8 *)(qrow + 16 * st + 8 * hi);
+    }
+    // K / V rows 0-63 (rows past the end: finite copies of the last row, masked /
+    // P = 0), K chunk j of row r at chunk j ^ ((r >> 1) & 7), V at j ^ (((r >> 1) & 1) << 2)
+    const h16 *kbase = qkv + (size_t)start * ld + d + h * DH;
+#pragma unroll
+    for (int k = 0; k < NK * 8 / 128; ++k) {
+        const int c = tid + 128 * k, r = c >> 3, j = c & 7;
+        const size_t so = (size_t)min(r, len - 1) * ld + 8 * j;
+        const uint4 kv = *(const uint4 *)(kbase + so);
+        const uint4 vv = *(const uint4 *)(kbase + d + so);
+        *(uint4 *)(smem + r * RB + ((j ^ ((r >> 1) & 7)) << 4)) = kv;
+        *(uint4 *)(smem + VB + r * RB + ((j ^ (((r >> 1) & 1) << 2)) << 4)) = vv;
+    }
+    __syncthreads();
+    if (32 * w >= len) return;                            // wave-uniform: no queries
+    const h16 s16 = (h16)sl2;
+    const h16x8 sc = {s16, s16, s16, s16, s16, s16, s16, s16};
+#pragma unroll
+    for (int st = 0; st < DH / 16; ++st) qf[st] *= sc;
+    // S^T = K Q^T for keys 0-63 (lds3 qk(0, false))
+    f32x16 s[2];
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[kh][r] = 0.f;
+#pragma unroll
+        for (int st = 0; st < DH / 16; ++st) {
+            const int ko = lq * RB + (((2 * st + hi) ^ ((lq >> 1) & 7)) << 4) + kh * 32 * RB;
+            const h16x8 a = *(const h16x8 *)(smem + ko);
+            s[kh] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, qf[st], s[kh], 0, 0, 0);
+        }
+    }
+    if (NK > len) {
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int key = 32 * kh + (r & 3) + 8 * (r >> 2) + 4 * hi;
+                if (key >= len) s[kh][r] = -INFINITY;
+            }
+    }
+    // the offset: the row max, f16-rounded; P = exp2(S - c); this half's sum
+    float mx = s[0][0];
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int r = (kh ? 0 : 1); r < 16; ++r) mx = fmaxf(mx, s[kh][r]);
+    const float c = (float)(h16)halves_max(mx);
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[kh][r] -= c;
+    float l = 0.f;
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float p = __builtin_amdgcn_exp2f(s[kh][r]);
+            s[kh][r] = p;
+            l += p;
+        }
+    // O^T = V^T P^T (lds3 pv(0))
+    const int gi = lane & 15, gq = gi >> 2, gp = gi & 3, gg = lane >> 4;
+    const int vsw = ((gq >> 1) & 1) << 2;
+    f32x16 o[DH / 32];
+#pragma unroll
+    for (int t = 0; t < DH / 32; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[t][r] = 0.f;
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            h16x8 bp;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) bp[j] = (h16)s[kh][8 * s2 + j];
+#pragma unroll
+            for (int t = 0; t < DH / 32; ++t) {
+                const int ch = 4 * t + 2 * (gg & 1) + (gp >> 1);
+                const char *va = smem + VB + (4 * (gg >> 1) + gq) * RB + ((ch ^ vsw) << 4) + 8 * (gp & 1) +
+                                 (32 * kh + 16 * s2) * RB;
+                const h16x4 lo = lds_read_tr16(va);
+                const h16x4 up = lds_read_tr16(va + 8 * RB);
+                const h16x8 a = {lo[0], lo[1], lo[2], lo[3], up[0], up[1], up[2], up[3]};
+                o[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bp, o[t], 0, 0, 0);
+            }
+        }
+    }
+    // rows out: lds3's store phase (1 / l, one permlane32 swap per dword of a
+    // chunk pair, four 16-B bounds-checked stores per lane; rows >= len dropped)
+    const float inv = 1.0f / halves_sum(l);
+    const int q = 32 * w + lq;
+    uint32_t pk[DH / 8][2];
+#pragma unroll
+    for (int m = 0; m < DH / 8; ++m)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int t = m >> 2, g = m & 3;
+            const h16x2 v = {(h16)(o[t][4 * g + 2 * k] * inv), (h16)(o[t][4 * g + 2 * k + 1] * inv)};
+            pk[m][k] = __builtin_bit_cast(uint32_t, v);
+        }
+#pragma unroll
+    for (int p = 0; p < DH / 16; ++p)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const auto r = __builtin_amdgcn_permlane32_swap(pk[2 * p][k], pk[2 * p + 1][k], false, false);
+            pk[2 * p][k] = r[0];
+            pk[2 * p + 1][k] = r[1];
+        }
+    const __amdgpu_buffer_rsrc_t ors =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(out + (size_t)start * d), (short)0, len * d * 2, 0x00020000);
+    const int ob = (q * d + h * DH + 8 * hi) * 2;
+#pragma unroll
+    for (int p = 0; p < DH / 16; ++p) {
+        typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+        const u32x4v v = {pk[2 * p][0], pk[2 * p][1], pk[2 * p + 1][0], pk[2 * p + 1][1]};
+        __builtin_amdgcn_raw_buffer_store_b128(v, ors, ob + 32 * p, 0, 0);
+    }
+}
 
 thread_local int g_att_variant = 0;   // benches only (bertx_bench_attention), per calling thread
+
+// BERT_ATT_SHORT=0: short batches through attention_lds3 as well (A/B)
+static bool att_short_env()
+{
+    static const bool on = [] { const char *e = std::getenv("BERT_ATT_SHORT"); return !(e && *e == '0'); }();
+    return on;
+}
 
 void launch_attention(const uint16_t *qkv, const int32_t *cu, int32_t n_seqs, int32_t max_len, int32_t n_head,
                       int32_t d, uint16_t *out, hipStream_t s)
@@ -706,6 +860,13 @@ void launch_attention(const uint16_t *qkv, const int32_t *cu, int32_t n_seqs, in
             // 0: production (attention_lds3, persistent, one workgroup per CU); 7:
             // the same kernel on at most 7 workgroups (tests: many ragged items each)
             const int n_items = n_seqs * n_head;
+            // short batches (max_len <= 64): one 2-wave workgroup per item, lds3's
+            // block-0 arithmetic (the same bits); variant 8 forces lds3 (tests, A/B)
+            if (max_len <= 64 && g_att_variant != 7 && g_att_variant != 8 && att_short_env()) {
+                if (n_items > 0)
+                    attention_short_kernel<<<n_items, 128, 0, s>>>((const h16 *)qkv, cu, d, n_head, sl2, (h16 *)out);
+                return;
+            }
             const int cap = g_att_variant == 7 ? 7 : device_cu_count();
             const int grid = n_items < cap ? n_items : cap;
             if (grid > 0)

@@ -387,6 +387,33 @@ def test_attention_matches_numpy(lib, variant, dh):
     assert err < 6e-3 * max(1.0, np.abs(ref).max()), err
 
 
+@pytest.mark.parametrize("seed", [0, 1])
+def test_short_attention_bitwise_equal_to_lds3(lib, seed):
+    """Batches of at most 64 tokens per sentence (the serving shape) run
+    attention_short_kernel: lds3's block-0 arithmetic on one 2-wave workgroup per
+    (sentence, head).  Against numpy, and bitwise equal to attention_lds3 forced on
+    the same batch (variant 8): a short sentence gets the same bits alone as inside
+    a batch with longer sentences (the forward's batch-composition invariance)."""
+    n_head, dh = 12, 64
+    d = n_head * dh
+    lens = [1, 2, 5, 31, 32, 33, 63, 64, 17]
+    cu = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    T = int(cu[-1])
+    rng = np.random.default_rng(seed)
+    qkv = (rng.standard_normal((T, 3 * d)) * (1.0 + 3.0 * seed)).astype(np.float16)
+    outs = {}
+    for variant in (0, 8):
+        out = np.zeros((T, d), np.float16)
+        rc = lib.bertx_test_attention(qkv.ctypes.data, cu.ctypes.data, len(lens), n_head, d, variant, out.ctypes.data)
+        assert rc == 0
+        outs[variant] = out
+    assert np.array_equal(outs[0].view(np.uint16), outs[8].view(np.uint16))
+    ref = attention_ref(qkv, cu, n_head, d)
+    got = outs[0].astype(np.float64)
+    assert np.isfinite(got).all()
+    assert np.abs(got - ref).max() < 6e-3 * max(1.0, np.abs(ref).max())
+
+
 @pytest.mark.parametrize("fmt", [1, 2, 3, 8])
 @pytest.mark.parametrize("cfg", [2, 3, 11, 16])
 def test_small_tiles_bitwise_equal_to_64x64(lib, fmt, cfg):
