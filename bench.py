@@ -373,6 +373,27 @@ def probes(lib, bertpy, torch, a, dev, stream, q4_path):
         except Exception as ex:
             out["q4_0_hbm"]["pmc"] = {"error": str(ex)}
     del f
+    # C1 (BASELINE.json configs[0]): all-MiniLM-L6-v2 f32, one sentence of 32 tokens --
+    # the reference's CPU plumbing case; here on the f32 chain (f32 activations x f32
+    # weights, f32.hip).  The CPU side of C1 is timed in the cpu_baseline leg.
+    try:
+        hp = bertpy.ARCHS["all-MiniLM-L6-v2"]
+        p1 = ensure_model(bertpy, a.model_dir, "all-MiniLM-L6-v2", "f32", a.seed)
+        f = DeviceForward(lib, bertpy, torch, p1, bertpy.synthetic_ids(1, 32, hp["n_vocab"], seed=7), dev, stream)
+        for _ in range(3):
+            f.step()
+        f.sync()
+        f.check()
+        n1 = max(200, steps)
+        el = timed_steps(f.step, n1, f.sync)
+        _, st = f.kernel_pass(n1)
+        out["c1_f32"] = {"workload": "C1 all-MiniLM-L6-v2 f32, B 1, L 32 (bertx_forward_device, the f32 chain)",
+                         "latency_us": round(el / n1 * 1e6, 1), "sentences_per_s": round(n1 / el, 1),
+                         "kernel_avg_us": {s["name"]: round(s["ms"] * 1e3 / s["launches"], 2)
+                                           for s in st if s["launches"]}}
+        del f
+    except Exception as ex:   # a probe is a report, never the metric
+        out["c1_f32"] = {"error": str(ex)}
     # the other two GPU configs of BASELINE.json at one GPU's share: C4 (bge-large q4_1,
     # L 512, 256 sentences over 8 GPUs = 32 per GPU: the replicas-only multi-GPU
     # path runs exactly this per GPU) and C5 (bge-base-zh q8_0, 128 ragged sentences)
@@ -756,6 +777,32 @@ def main():
                                    "gpu_vs_cpu_min_cosine": round(cos, 6)}
         except Exception as ex:  # the baseline is a report, never the product
             res["cpu_baseline"] = {"value": None, "error": str(ex)}
+        if not a.no_probes:
+            # C1 (BASELINE.json configs[0], the reference's CPU case): all-MiniLM-L6-v2
+            # f32, one 32-token sentence, the oracle on this job's CPU share against the
+            # GPU's f32 chain through bert_forward_batch (the probes time the GPU side)
+            try:
+                import oracle_lib
+                share = len(os.sched_getaffinity(0))
+                n_thr = max(1, min(share, int(os.environ.get("OMP_NUM_THREADS", share))))
+                hp1 = bertpy.ARCHS["all-MiniLM-L6-v2"]
+                p1 = ensure_model(bertpy, a.model_dir, "all-MiniLM-L6-v2", "f32", a.seed)
+                ids1 = bertpy.synthetic_ids(1, 32, hp1["n_vocab"], seed=7)
+                g1 = bertpy.BertModel(p1, lib=lib).forward_batch(ids1)
+                o1 = oracle_lib.Oracle(p1)
+                o1.forward_batch(ids1, n_threads=n_thr)          # warm (page-in, tables)
+                reps = 20
+                c0 = time.perf_counter()
+                for _ in range(reps):
+                    c1e = o1.forward_batch(ids1, n_threads=n_thr)
+                c1 = time.perf_counter()
+                res["cpu_baseline"]["c1"] = {
+                    "workload": "C1 all-MiniLM-L6-v2 f32, B 1, L 32: the C oracle (f32 x f32, as the reference's "
+                                "f32 path) on this job's CPU share",
+                    "cpu_ms_per_sentence": round((c1 - c0) / reps * 1e3, 3), "cores": n_thr,
+                    "gpu_vs_cpu_cosine": round(float(np.sum(g1[0] * c1e[0])), 9)}
+            except Exception as ex:   # a report, never the product
+                res["cpu_baseline"]["c1"] = {"error": str(ex)}
 
     if rank == 0 and world == 1 and not a.no_probes and lib is not None:
         try:
