@@ -401,52 +401,7 @@ bool Device::finish_load()
         return false;
     }
     uploading_ = false;
-    if (!expand_small_batch_weights()) return false;
     ok_ = true;
-    return true;
-}
-
-// Small batches run QKV and FFN-up latency-bound (one wave per SIMD, the tile
-// config 16 K loop), where the in-register dequantization is a large part of
-// each K-step: there the GEMMs read an f16 expansion of the quantized weights,
-// made once here by the GEMM's own dequantization (launch_expand_f16), so the
-// f16 values multiplied -- and every output bit -- are those of the quantized
-// form.  2 (N_qkv + N_up) K bytes per layer.  BERT_SMALL_F16=0: off (A/B).
-bool Device::expand_small_batch_weights()
-{
-    static const bool on = [] { const char *e = std::getenv("BERT_SMALL_F16"); return !(e && *e == '0'); }();
-    if (!on || f32_ || wfmt_ == FMT_F16 || layers_.empty()) return true;
-    size_t bytes = 0;
-    for (const DevLayer &L : layers_)
-        bytes += (size_t)2 * ((size_t)L.qkv.N * L.qkv.K + (size_t)L.up.N * L.up.K);
-    if (hipMalloc((void **)&exp16_, bytes) != hipSuccess) {
-        (void)hipGetLastError();
-        exp16_ = nullptr;
-        trace("libbert: device %d: no room for the small-batch f16 weights (%zu bytes); quantized GEMMs only\n",
-              ordinal_, bytes);
-        return true;   // an optimisation, not a requirement
-    }
-    exp16_bytes_ = bytes;
-    size_t off = 0;
-    auto expand = [&](const DevWeight &q, DevWeight &h) {
-        h = q;
-        h.fmt = FMT_F16;
-        h.qs = exp16_ + off;
-        h.d = h.m = nullptr;
-        off += (size_t)2 * q.N * q.K;
-        return launch_expand_f16(q, (uint16_t *)h.qs, stream_) == 0;
-    };
-    for (DevLayer &L : layers_)
-        if (!expand(L.qkv, L.qkv16) || !expand(L.up, L.up16)) {
-            errorf("libbert: f16 expansion of the weights failed on device %d\n", ordinal_);
-            return false;
-        }
-    const hipError_t e = hipStreamSynchronize(stream_);
-    if (e != hipSuccess) {
-        (void)hipGetLastError();
-        errorf("libbert: f16 expansion of the weights failed on device %d: %s\n", ordinal_, hipGetErrorString(e));
-        return false;
-    }
     return true;
 }
 
@@ -460,7 +415,6 @@ Device::~Device()
     for (auto &p : pending_) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (auto e : free_events_) (void)hipEventDestroy(e);
     if (arena_) (void)hipFree(arena_);
-    if (exp16_) (void)hipFree(exp16_);
     if (ws_) (void)hipFree(ws_);
     if (h_ids_) (void)hipHostFree(h_ids_);
     if (h_cu_) (void)hipHostFree(h_cu_);
@@ -696,13 +650,6 @@ int Device::forward_ordered(const int32_t *d_ids, const int32_t *d_cu, int n_seq
     return hipGraphLaunch(exec, s) == hipSuccess ? 0 : -1;
 }
 
-// The weight a projection of M rows reads: the f16 expansion where the launch takes
-// the latency-bound small-batch tile form (config 16), else the quantized weight.
-static const DevWeight &small_w(const DevWeight &q, const DevWeight &h16, int M)
-{
-    return (h16.qs && gemm_forward_cfg(q.N, M) == 16) ? h16 : q;
-}
-
 int Device::launch_all(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, int max_len, int T, float *d_out,
                        hipStream_t s, bool check)
 {
@@ -757,7 +704,7 @@ int Device::launch_all(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, in
         }
         in.c1 = L.c1_qkv;
         begin(K_GEMM_QKV, s, ev);
-        if (launch_gemm(small_w(L.qkv, L.qkv16, M), z_, M, L.c2_qkv, EPI_BIAS_F16, nullptr, qkv_, s, in) != 0) return -1;
+        if (launch_gemm(L.qkv, z_, M, L.c2_qkv, EPI_BIAS_F16, nullptr, qkv_, s, in) != 0) return -1;
         end(K_GEMM_QKV, s, ev, 2.0 * t * 3.0 * d * d);
         chk("gemm_qkv", l, qkv_, (size_t)T * 3 * d, 1);
 
@@ -788,7 +735,7 @@ int Device::launch_all(const int32_t *d_ids, const int32_t *d_cu, int n_seqs, in
         }
         in.c1 = L.c1_up;
         begin(K_GEMM_FFN_UP, s, ev);
-        if (launch_gemm(small_w(L.up, L.up16, M), z_, M, L.c2_up, EPI_BIAS_GELU_F16, nullptr, ffn_, s, in) != 0) return -1;
+        if (launch_gemm(L.up, z_, M, L.c2_up, EPI_BIAS_GELU_F16, nullptr, ffn_, s, in) != 0) return -1;
         end(K_GEMM_FFN_UP, s, ev, 2.0 * t * d * f);
         chk("gemm_up", l, ffn_, (size_t)T * f, 1);
 

@@ -29,10 +29,6 @@ struct KStats {
 
 struct DevLayer {
     DevWeight qkv, o, up, down;
-    // small batches (the latency-bound tile form): QKV and FFN-up on the f16
-    // expansion of their quantized weights (launch_expand_f16: the same f16 values,
-    // the same bits); empty for f16 / f32 files
-    DevWeight qkv16, up16;
     float *b_o = nullptr, *b_down = nullptr;
     // LN fold (kernels.h) of the projections that read a LayerNorm'd stream:
     // c1 = W gamma, c2 = b + W beta of the LN in front (QKV: the previous layer's
@@ -187,7 +183,6 @@ private:
                        hipStream_t s);
     void drop_graphs();
     void bind(const ModelImage &img);   // device pointers of the image's planes
-    bool expand_small_batch_weights();  // DevLayer::qkv16 / up16 (finish_load)
     bool uploading_ = false;
     void begin(int cls, hipStream_t s, hipEvent_t &a);
     void end(int cls, hipStream_t s, hipEvent_t a, double work);
@@ -201,8 +196,6 @@ private:
 
     // weights
     char *arena_ = nullptr;
-    char *exp16_ = nullptr;         // f16 expansions of QKV and FFN-up (DevLayer::qkv16, up16)
-    size_t exp16_bytes_ = 0;
     size_t arena_size_ = 0, arena_used_ = 0;
     DevTable word_, type_, pos_;
     float *ln_e_w_ = nullptr, *ln_e_b_ = nullptr;

@@ -842,40 +842,6 @@ int launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, i
 
 }  // namespace
 
-// f16 expansion of a quantized weight (small batches, engine.cpp): every lane
-// record's four A fragments exactly as the GEMM dequantizes them (ZRegs::frag:
-// (q - 8) d, q d + m, q d rounded once), written in the f16 lane-order layout, so a
-// GEMM on the expansion multiplies the same f16 values -- the same bits.
-template <int FMT>
-__global__ __launch_bounds__(256) void expand_f16_kernel(DevWeight W, uint4 *__restrict__ out, int64_t n_rec)
-{
-    const int64_t rec = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (rec >= n_rec) return;
-    const int64_t per_ks = (int64_t)(W.N / 32) * 64;
-    const int64_t ks = rec / per_ks, r2 = rec - ks * per_ks;
-    const int grp = (int)(r2 >> 6), fr = (int)(r2 & 15);
-    constexpr int QB = ZRegs<FMT>::QB;
-    const size_t so = (size_t)ks * 2 * W.N + ((size_t)grp * 16 + fr) * 4;
-    ZRegs<FMT> r;
-    r.load((const uint8_t *)W.qs + rec * QB, W.d + so, FMT == FMT_Q4_1 ? W.m + so : nullptr);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) out[rec * 4 + u] = __builtin_bit_cast(uint4, r.frag(u));
-}
-
-int launch_expand_f16(const DevWeight &W, uint16_t *out, hipStream_t s)
-{
-    if (W.N % 32 || W.K % ZK || W.kx) return -1;
-    const int64_t n_rec = (int64_t)(W.K / ZK) * (W.N / 32) * 64;
-    const unsigned grid = (unsigned)((n_rec + 255) / 256);
-    switch (W.fmt) {
-    case FMT_Q4_0: expand_f16_kernel<FMT_Q4_0><<<grid, 256, 0, s>>>(W, (uint4 *)out, n_rec); break;
-    case FMT_Q4_1: expand_f16_kernel<FMT_Q4_1><<<grid, 256, 0, s>>>(W, (uint4 *)out, n_rec); break;
-    case FMT_Q8_0: expand_f16_kernel<FMT_Q8_0><<<grid, 256, 0, s>>>(W, (uint4 *)out, n_rec); break;
-    default: return -1;
-    }
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
 thread_local int g_gemm_cfg = 0;
 thread_local int g_gemm_ran = 0;
 
@@ -891,8 +857,6 @@ bool gemm_fold_ok(const DevWeight &W, int32_t M, int32_t G)
 {
     return G > 0 && M > 0 && M % 64 == 0 && 32 * G == (W.kx ? W.kx : W.K) && G <= fold_cap(pick_cfg(W.N, M, forward_cfg()));
 }
-
-int gemm_forward_cfg(int32_t N, int32_t M) { return pick_cfg(N, M, forward_cfg()); }
 
 // CUs of the calling thread's current device, cached per ordinal (a context may
 // hold devices in different partition modes; launches size persistent grids

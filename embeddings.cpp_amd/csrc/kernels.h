@@ -111,13 +111,6 @@ bool gemm_fold_ok(const DevWeight &W, int32_t M, int32_t G);
 
 // CU count of the calling thread's current HIP device (cached per ordinal).
 int device_cu_count();
-// The tile config a forward launch of width N over M rows takes (gemm.hip
-// launch_fmt: 2, 3, 4, 16 -- 16 is the latency-bound small-batch form).
-int gemm_forward_cfg(int32_t N, int32_t M);
-// f16 expansion of a quantized W (q4_0 / q4_1 / q8_0) into out (K x N f16, the f16
-// lane-order layout): the exact f16 A fragments the GEMM dequantizes, so a GEMM on
-// it gives the same bits.  -1 for an unsupported weight.
-int launch_expand_f16(const DevWeight &W, uint16_t *out, hipStream_t s);
 
 // z = f16((pos[i] + (type[0] + word[id])) * gamma) and the (mean, 1/sigma) of
 // the f32 sum, for every valid token (bert.cpp:963-984).

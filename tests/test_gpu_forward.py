@@ -514,3 +514,22 @@ print("FWD", bool(np.isfinite(e).all()), flush=True)
     text = log.read_text()
     assert f"BERT_FAULT_INJECT={stage}" in text, text
     assert "SECOND 4" in out and "FWD True" in out, out
+
+
+@pytest.mark.parametrize("ftype", ["q4_0", "q4_1", "q8_0"])
+def test_short_sentences_bitwise_across_tile_forms(tmp_path, ftype):
+    """A short sentence alone (64 GEMM rows: the small-batch tile form 16, wave-private
+    X rings; max_len <= 64: the short attention kernel) has the bits it has inside a
+    large batch (256- and 128-row tiles, the persistent attention), for every
+    quantized format at MiniLM dims (d 384, 12 heads of 32).
+    Round 6 also ran an f16 expansion of the QKV / FFN-up weights for the small
+    form under this test (bitwise, but slower: profiles/r06_small_f16_expansion_ab.log)."""
+    path = str(tmp_path / f"minilm-{ftype}.bin")
+    bertpy.synthetic_model(path, "all-MiniLM-L6-v2", ftype, seed=1234)
+    m = bertpy.BertModel(path)
+    short = ragged_ids(30522, [5, 32, 60], seed=8)
+    big = ragged_ids(30522, [512] * 16, seed=9)
+    full = m.forward_batch(short + big)
+    for i, s in enumerate(short):
+        assert np.array_equal(m.forward_batch([s])[0], full[i]), (ftype, len(s))
+    assert np.array_equal(m.forward_batch(short), full[:3])
