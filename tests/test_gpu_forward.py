@@ -519,9 +519,9 @@ print("FWD", bool(np.isfinite(e).all()), flush=True)
 @pytest.mark.parametrize("ftype", ["q4_0", "q4_1", "q8_0"])
 def test_short_sentences_bitwise_across_tile_forms(tmp_path, ftype):
     """A short sentence alone (64 GEMM rows: the small-batch tile form 16, wave-private
-    X rings; max_len <= 64: the short attention kernel) has the bits it has inside a
-    large batch (256- and 128-row tiles, the persistent attention), for every
-    quantized format at MiniLM dims (d 384, 12 heads of 32).
+    X rings) has the bits it has inside a large batch (256- and 128-row tiles), for
+    every quantized format at MiniLM dims (d 384, 12 heads of 32; the dh-64 short
+    attention kernel has its own bitwise test, test_short_attention_bitwise_equal_to_lds3).
     Round 6 also ran an f16 expansion of the QKV / FFN-up weights for the small
     form under this test (bitwise, but slower: profiles/r06_small_f16_expansion_ab.log)."""
     path = str(tmp_path / f"minilm-{ftype}.bin")
