@@ -331,7 +331,7 @@ bool build_model_image(const HostModel &m, ModelImage &img, std::string &err, bo
         // one async copy on its own stream; pieces are freed as they are copied
         uint8_t *dst = nullptr;
         if (pin) {
-            if (hipHostMalloc((void **)&img.pinned_, img.total, hipHostMallocDefault) != hipSuccess) {
+            if (hipHostMalloc((void **)&img.pinned_, img.total, hipHostMallocPortable) != hipSuccess) {   // every device copies from it
                 (void)hipGetLastError();
                 img.pinned_ = nullptr;
                 trace("build_model_image: page-locking %zu bytes failed, pageable uploads\n", img.total);
