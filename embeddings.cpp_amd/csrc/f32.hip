@@ -128,13 +128,18 @@ __device__ __forceinline__ float era_table(const uint16_t *__restrict__ tab, flo
     return (float)as_h(tab[__builtin_bit_cast(uint16_t, (h16)v)]);
 }
 
-// Y[m][n] = epi(sum_k X[m][k] W[n][k]) on 64 x 64 tiles, 4 waves of 32 x 32
-// (2 x 2 v_mfma_f32_16x16x4_f32 tiles each), K in steps of 32 through
-// LDS (rows padded to 33 floats).  A = X (lane: row l & 15, k = l >> 4), B = W^T
-// (k = l >> 4, feature l & 15); D lane: feature l & 15, tokens 4 (l >> 4) + r.
+// Y[m][n] = epi(sum_k X[m][k] W[n][k]) on 64 x 32 tiles, 4 waves of 32 x 16
+// (2 v_mfma_f32_16x16x4_f32 tiles each), K in steps of 32 through LDS (rows
+// padded to 33 floats), the next step's words loaded during this step's MFMAs.
+// A = X (lane: row l & 15, k = l >> 4), B = W^T (k = l >> 4, feature l & 15); D
+// lane: feature l & 15, tokens 4 (l >> 4) + r.  Every output is one k-ordered
+// MFMA chain whatever the tile shape (so a sentence's bits do not depend on its
+// batch); the tile is narrow because the f32 chain's batches are small (C1: one
+// sentence): twice the workgroups of a 64 x 64 tile and half the MFMAs per wave
+// and K-step (C1 711 -> 527 us with the double buffer alone).
 // EPI: 0 bias + acc, 1 GELU table(bias + acc), 2 (bias + acc) + res (the
 // reference's operand order, bert.cpp:1040-1045, 1066-1072).
-constexpr int F32_BK = 32;
+constexpr int F32_BK = 32, F32_BN = 32;
 
 template <int EPI>
 __global__ __launch_bounds__(256) void f32_gemm_kernel(const float *__restrict__ X, const float *__restrict__ W,
@@ -142,60 +147,58 @@ __global__ __launch_bounds__(256) void f32_gemm_kernel(const float *__restrict__
                                                        float *__restrict__ Y, int N, int K, int nN,
                                                        const uint16_t *__restrict__ gelu_tab)
 {
-    __shared__ float xs[64][F32_BK + 1], ws[64][F32_BK + 1];
+    __shared__ float xs[64][F32_BK + 1], ws[F32_BN][F32_BK + 1];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int m0 = (blockIdx.x / nN) * 64, n0 = (blockIdx.x % nN) * 64;
-    const int wm = (w >> 1) * 32, wn = (w & 1) * 32;
-    const int lr = tid >> 2, lc = (tid & 3) * 8;   // loader: row lr, columns lc .. lc + 7
-    const bool wrow = n0 + lr < N;
-    f32x4 acc[2][2];
+    const int m0 = (blockIdx.x / nN) * 64, n0 = (blockIdx.x % nN) * F32_BN;
+    const int wm = (w >> 1) * 32, wn = (w & 1) * 16;
+    const int lr = tid >> 2, lc = (tid & 3) * 8;     // X loader: row lr, columns lc .. lc + 7
+    const int wr = tid >> 3, wc = (tid & 7) * 4;     // W loader: row wr, columns wc .. wc + 3
+    const bool wrow = n0 + wr < N;
+    f32x4 acc[2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 2; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     const float *xp = X + (size_t)(m0 + lr) * K + lc;
-    const float *wp = W + (size_t)(wrow ? n0 + lr : 0) * K + lc;
+    const float *wp = W + (size_t)(wrow ? n0 + wr : 0) * K + wc;
+    f32x4 x0 = *(const f32x4 *)xp, x1 = *(const f32x4 *)(xp + 4);
+    f32x4 w0 = {0.f, 0.f, 0.f, 0.f};
+    if (wrow) w0 = *(const f32x4 *)wp;
     for (int k0 = 0; k0 < K; k0 += F32_BK) {
-        const f32x4 x0 = *(const f32x4 *)(xp + k0), x1 = *(const f32x4 *)(xp + k0 + 4);
-        f32x4 w0 = {0.f, 0.f, 0.f, 0.f}, w1 = w0;
-        if (wrow) { w0 = *(const f32x4 *)(wp + k0); w1 = *(const f32x4 *)(wp + k0 + 4); }
         __syncthreads();   // the previous step's fragment reads are done
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             xs[lr][lc + e] = x0[e]; xs[lr][lc + 4 + e] = x1[e];
-            ws[lr][lc + e] = w0[e]; ws[lr][lc + 4 + e] = w1[e];
+            ws[wr][wc + e] = w0[e];
         }
         __syncthreads();
+        if (k0 + F32_BK < K) {
+            const int kn = k0 + F32_BK;
+            x0 = *(const f32x4 *)(xp + kn);
+            x1 = *(const f32x4 *)(xp + kn + 4);
+            if (wrow) w0 = *(const f32x4 *)(wp + kn);
+        }
 #pragma unroll
         for (int kk = 0; kk < F32_BK; kk += 4) {
-            float a[2], bq[2];
+            const float bq = ws[wn + (lane & 15)][kk + (lane >> 4)];
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                a[i] = xs[wm + 16 * i + (lane & 15)][kk + (lane >> 4)];
-                bq[i] = ws[wn + 16 * i + (lane & 15)][kk + (lane >> 4)];
+                const float a = xs[wm + 16 * i + (lane & 15)][kk + (lane >> 4)];
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bq, acc[i], 0, 0, 0);
             }
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], bq[j], acc[i][j], 0, 0, 0);
         }
     }
+    const int n = n0 + wn + (lane & 15);
+    if (n >= N) return;
+    const float bv = bias[n];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const int n = n0 + wn + 16 * j + (lane & 15);
-        if (n >= N) continue;
-        const float bv = bias[n];
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const size_t o = (size_t)(m0 + wm + 16 * i + 4 * (lane >> 4) + r) * N + n;
-                float v = bv + acc[i][j][r];
-                if (EPI == 1) v = era_table(gelu_tab, v);
-                if (EPI == 2) v = v + res[o];
-                Y[o] = v;
-            }
-    }
+        for (int r = 0; r < 4; ++r) {
+            const size_t o = (size_t)(m0 + wm + 16 * i + 4 * (lane >> 4) + r) * N + n;
+            float v = bv + acc[i][r];
+            if (EPI == 1) v = era_table(gelu_tab, v);
+            if (EPI == 2) v = v + res[o];
+            Y[o] = v;
+        }
 }
 
 // ---------------------------------------------------------------- attention
@@ -296,8 +299,11 @@ __global__ __launch_bounds__(256) void f32_pool_kernel(const float *__restrict__
     for (int j = 0; j < 4; ++j) {
         const int c = tid + 256 * j;
         float a = 0.f;
-        if (c < d)
+        if (c < d) {
+            // (unrolled: eight loads in flight; the fmaf chain keeps its token order)
+#pragma unroll 8
             for (int i = 0; i < len; ++i) a = fmaf(x[(size_t)(start + i) * d + c], wt, a);
+        }
         e[j] = a;
         ss += (double)(a * a);
     }
@@ -332,7 +338,7 @@ int launch_f32_gemm(const float *X, int32_t M, const float *W, int32_t N, int32_
     if (M % 64 || K % F32_BK || N <= 0 || M <= 0 || epi < 0 || epi > 2 || (epi == 2 && !res) ||
         (epi == 1 && !gelu_tab))
         return -1;
-    const int nN = (N + 63) / 64, grid = (M / 64) * nN;
+    const int nN = (N + F32_BN - 1) / F32_BN, grid = (M / 64) * nN;
     if (epi == 0) f32_gemm_kernel<0><<<grid, 256, 0, s>>>(X, W, bias, res, Y, N, K, nN, gelu_tab);
     else if (epi == 1) f32_gemm_kernel<1><<<grid, 256, 0, s>>>(X, W, bias, res, Y, N, K, nN, gelu_tab);
     else f32_gemm_kernel<2><<<grid, 256, 0, s>>>(X, W, bias, res, Y, N, K, nN, gelu_tab);
