@@ -533,3 +533,20 @@ def test_short_sentences_bitwise_across_tile_forms(tmp_path, ftype):
     for i, s in enumerate(short):
         assert np.array_equal(m.forward_batch([s])[0], full[i]), (ftype, len(s))
     assert np.array_equal(m.forward_batch(short), full[:3])
+
+
+def test_load_free_cycles_multi_replica(quant_models, monkeypatch):
+    """The load path that aborted on round 5's driver box, exercised repeatedly: ten
+    cycles of a 4-replica context on one GPU (load, a small forward on the routed
+    replica, free), each bitwise the single-replica result.  Every HIP call of a
+    load now runs on the loading thread."""
+    path = quant_models[("tiny64", "q8_0")]
+    ids = ragged_ids(690, [7, 64, 200], seed=12)
+    monkeypatch.setenv("BERT_DEVICES", "0")
+    want = bertpy.BertModel(path).forward_batch(ids)
+    monkeypatch.setenv("BERT_DEVICES", "0,0,0,0")
+    for _ in range(10):
+        m = bertpy.BertModel(path)
+        assert m.lib.bertx_num_devices(m.ctx) == 4
+        assert np.array_equal(m.forward_batch(ids), want)
+        del m
