@@ -402,10 +402,12 @@ static bert_ctx *load_context(const char *fname)
                     "compute path (set BERT_HOST_ONLY=1 for a tokenizer-only context)\n");
         return nullptr;
     }
+    ctx->devices.reserve(devs.size());
     for (size_t i = 0; i < devs.size(); ++i) {
         if (devs.size() > 1) emb::trace("bert_load_from_file: replica %zu on device %d: create + upload\n", i, devs[i]);
         if (i == 1 && emb::fault_inject("replica1")) throw std::runtime_error("BERT_FAULT_INJECT=replica1");
-        ctx->devices.emplace_back(new Device(devs[i], img));
+        std::unique_ptr<Device> d(new Device(devs[i], img));   // owned before anything else can throw
+        ctx->devices.push_back(std::move(d));
     }
     bool ok = true;
     for (auto &d : ctx->devices) {
@@ -419,7 +421,11 @@ static bert_ctx *load_context(const char *fname)
     ctx->inflight.assign(ctx->devices.size(), 0.0);
     if (ctx->devices.size() > 1) {
         if (emb::fault_inject("worker")) throw std::system_error(std::make_error_code(std::errc::resource_unavailable_try_again), "BERT_FAULT_INJECT=worker");
-        for (size_t i = 0; i < ctx->devices.size(); ++i) ctx->workers.emplace_back(new ReplicaWorker());
+        ctx->workers.reserve(ctx->devices.size());
+        for (size_t i = 0; i < ctx->devices.size(); ++i) {
+            std::unique_ptr<ReplicaWorker> w(new ReplicaWorker());   // joined by its destructor on any unwind
+            ctx->workers.push_back(std::move(w));
+        }
     }
     emb::infof("bert_load_from_file: MI355X engine on %zu HIP device(s)\n", ctx->devices.size());
     if (m.hp.ftype == emb::FMT_F32)
