@@ -332,7 +332,7 @@ def test_oracle_pinned_to_torch_at_survey_dims(oracle, tmp_path, arch, ftype, pr
     SURVEY architectures (the committed goldens pin it on tiny models only): C1's
     MiniLM-L6 f32 file on sharp weights, and C3's bge-base architecture as a q4_0 file
     -- torch runs the file's dequantized weights (embedding tables included) and the
-    oracle runs its f32-activation switch, so both multiply the same weights by f32
+    oracle runs its f32-activation mode, so both multiply the same weights by f32
     activations and the comparison pins the oracle's q4_0 decoding, layer order, era
     GELU / softmax tables and pooling at full depth.  Ragged lengths (padding and mask)."""
     import bertpy
