@@ -215,12 +215,18 @@ def test_bge_base_q4_0_full_size(tmp_path):
     full = m.forward_batch(ids)
     assert np.all(np.isfinite(full))
     assert np.allclose(np.linalg.norm(full, axis=1), 1.0, atol=1e-5)
+    # captured on the second run, replayed on the third: the in-launch statistics'
+    # flags (cleared by the residual GEMM in front of each projection) hold across
+    # replays
+    assert np.array_equal(m.forward_batch(ids), full)
+    assert np.array_equal(m.forward_batch(ids), full)
     two = m.forward_batch(ids[:2])
     assert np.array_equal(two, full[:2])
     assert np.array_equal(m.forward_batch(ids[62:]), full[62:])
     # every sentence bitwise as in 8-sentence batches (those launch one workgroup
-    # per tile; the full batch runs its N = 768 GEMMs persistent, two workgroups
-    # per CU walking the tiles: gemm.hip dispatch_z)
+    # per tile and an ln_stats launch in front of each projection; the full batch
+    # runs its N = 768 GEMMs persistent, two workgroups per CU walking the tiles,
+    # and its projections with in-launch statistics: gemm.hip dispatch_z)
     eights = np.concatenate([m.forward_batch(ids[i:i + 8]) for i in range(0, 64, 8)])
     assert np.array_equal(eights, full)
     ref = oracle_lib.Oracle(path).forward_batch([ids[0], ids[1], ids[63]], n_threads=min(16, os.cpu_count() or 1))
