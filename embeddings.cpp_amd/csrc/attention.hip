@@ -3,6 +3,7 @@
 #include "diag_att_stamps.h"
 #include "kernels.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <utility>
@@ -840,6 +841,282 @@ __global__ __launch_bounds__(128) void attention_short_kernel(const h16 *__restr
     }
 }
 
+// ---------------------------------------------------------------------------
+// attention_pp (production for 64 < L <= 512, dh 64; round 6): lds3's per-query
+// arithmetic in two co-resident 8-wave workgroups per CU instead of one 16-wave
+// workgroup, so one workgroup's per-unit phases (Q in, block 0, the row stores)
+// run beside the other's steady blocks instead of stalling the whole CU.  A unit is
+// half an item: 256 queries (8 waves x 32, wave w of half qh = lds3's wave
+// 8 qh + w) over all of the sentence's keys; K and V stream through a 4-stage
+// LDS ring of 64-key blocks (16 KiB a stage: 64 KiB per workgroup, two per CU),
+// each wave issuing one K and one V piece per block, NS - 1 blocks ahead; a
+// barrier per block publishes block j and frees block j - 1's stage.  The two
+// halves of an item are consecutive units on one XCD, so the second reads K/V
+// from that L2.  Every query runs lds3's block sequence (block 0 sets the f16
+// offset, later blocks the biased QK^T, the ballot rescale, P.V) on the same
+// wave composition, so the output has lds3's bits (the kernel tests compare them).
+// (Round 6 also measured, all bitwise equal and slower: four 4-wave workgroups
+// per CU with a 2-stage ring, a barrier per block pair, and a persistent form
+// whose ring runs on across units; profiles/r06_attention_pp_ab.log.)
+__global__ __launch_bounds__(512, 4) void attention_pp_kernel(const h16 *__restrict__ qkv,
+                                                              const int32_t *__restrict__ cu, int d, int nh,
+                                                              float sl2, h16 *__restrict__ out)
+{
+    constexpr int NW = 8, NS = 4, DH = 64, RB = DH * 2, SB = 2 * 64 * RB, VO = 64 * RB;
+    constexpr int UPI = 16 / NW, PW = 16 / NW;            // units per item, pieces per wave and block
+    __shared__ __attribute__((aligned(16))) char smem[NS * SB];
+    const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int hi = lane >> 5, lq = lane & 31;
+    const int ld = 3 * d;
+    // XCD-aware bijective remap (as the GEMM tiles): each XCD a contiguous run of
+    // units, so an item's two halves share its L2
+    const int nb = gridDim.x, bid = blockIdx.x, xcd = bid & 7, qq = nb >> 3, rr = nb & 7;
+    const int u = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+    const int it = u / UPI, q0 = 32 * NW * (u - it * UPI);
+    const int b = it / nh, h = it - b * nh;
+    const int start = cu[b], len = cu[b + 1] - start;
+    if (q0 >= len) return;                                // workgroup-uniform: no queries
+    const int nblk = (len + 63) >> 6;
+    const bool active = q0 + 32 * w < len;                // wave-uniform
+    const h16 *kbase = qkv + (size_t)start * ld + d + h * DH;
+
+    // block j's K and V rows into stage j % NS: piece i < 8 is K rows 8i .. 8i + 7
+    // of the block, 8 + i the same V rows (K swizzled by (row >> 1) & 7, V by
+    // ((row >> 1) & 1) << 2, the row's parity within the block being its parity in
+    // the sentence); wave w issues pieces w, w + NW, ...; rows past the end are
+    // finite copies (masked / P = 0)
+    auto issue = [&](int j) {
+        const int ln = lane_id_opaque();
+#pragma unroll
+        for (int k = 0; k < PW; ++k) {
+            const int i = w + NW * k, r8 = i & 7;
+            const int row = 64 * j + 8 * r8 + (ln >> 3), pc = ln & 7;
+            const size_t so = (size_t)min(row, len - 1) * ld;
+            char *dst = smem + (j % NS) * SB + i * 1024;
+            if (i < 8) glds16_hidden(kbase + so + (pc ^ ((row >> 1) & 7)) * 8, dst);
+            else glds16_hidden(kbase + d + so + (pc ^ (((row >> 1) & 1) << 2)) * 8, dst);
+        }
+    };
+    // the wave's Q rows by asm loads (hipcc's waitcnt pass does not see them, so it
+    // puts no vmcnt(0) at their first use, which would retire every prologue
+    // piece); then blocks 0-2 (always three: a block past the sentence is a
+    // clamped copy into a stage no block reads), so block 0's wait below has one
+    // constant count and is one asm tied to the Q registers (a wait per branch
+    // let hipcc copy the registers in front of it, before the loads landed)
+    h16x8 qf[DH / 16];
+    {
+        const h16 *qrow = qkv + (size_t)(start + min(q0 + 32 * w + lq, len - 1)) * ld + h * DH;
+#pragma unroll
+        for (int st = 0; st < DH / 16; ++st)
+            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qf[st]) : "v"(qrow + 16 * st + 8 * hi) : "memory");
+    }
+#pragma unroll
+    for (int j = 0; j < NS - 1; ++j) issue(j);
+
+    // lane-constant LDS offsets within a stage (lds3's)
+    int koff[DH / 16];
+#pragma unroll
+    for (int st = 0; st < DH / 16; ++st) koff[st] = lq * RB + (((2 * st + hi) ^ ((lq >> 1) & 7)) << 4);
+    const int gi = lane & 15, gq = gi >> 2, gp = gi & 3, gg = lane >> 4;
+    const int vsw = ((gq >> 1) & 1) << 2;
+    int voff[DH / 32];
+#pragma unroll
+    for (int t = 0; t < DH / 32; ++t) {
+        const int ch = 4 * t + 2 * (gg & 1) + (gp >> 1);
+        voff[t] = (4 * (gg >> 1) + gq) * RB + ((ch ^ vsw) << 4) + 8 * (gp & 1) + VO;
+    }
+    const h16 one = (h16)1.0f, zero = (h16)0.0f;
+    const h16x8 abias = {hi ? zero : one, zero, zero, zero, zero, zero, zero, zero};
+    h16x8 bbias = {zero, zero, zero, zero, zero, zero, zero, zero};
+    f32x16 o[DH / 32];
+    float c = 0.f, l = 0.f;
+    f32x16 s[2];
+
+    auto qk = [&](int kb, int sbase, bool bias) {
+        int kbo[DH / 16];
+#pragma unroll
+        for (int st = 0; st < DH / 16; ++st) {
+            kbo[st] = koff[st] + sbase;
+            asm volatile("" : "+v"(kbo[st]));
+        }
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) {
+            if (bias) {
+                s[kh] = __builtin_amdgcn_mfma_f32_32x32x16_f16(abias, bbias, f32x16{}, 0, 0, 0);
+            } else {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) s[kh][r] = 0.f;
+            }
+#pragma unroll
+            for (int st = 0; st < DH / 16; ++st) {
+                const h16x8 a = *(const h16x8 *)(smem + kbo[st] + kh * 32 * RB);
+                s[kh] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, qf[st], s[kh], 0, 0, 0);
+            }
+        }
+        if (kb + 64 > len) {
+#pragma unroll
+            for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int key = kb + 32 * kh + (r & 3) + 8 * (r >> 2) + 4 * hi;
+                    if (key >= len) s[kh][r] = -INFINITY;
+                }
+        }
+    };
+    auto row_max = [&]() {
+        float mx = s[0][0];
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+            for (int r = (kh ? 0 : 1); r < 16; ++r) mx = fmaxf(mx, s[kh][r]);
+        return halves_max(mx);
+    };
+    auto shift_by = [&](float sh) {
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[kh][r] -= sh;
+    };
+    auto expsum = [&]() {
+        float rs = 0.f;
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float p = __builtin_amdgcn_exp2f(s[kh][r]);
+                s[kh][r] = p;
+                rs += p;
+            }
+        return rs;
+    };
+    auto pv = [&](int sbase) {
+        int vbo[DH / 32];
+#pragma unroll
+        for (int t = 0; t < DH / 32; ++t) {
+            vbo[t] = voff[t] + sbase;
+            asm volatile("" : "+v"(vbo[t]));
+        }
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) {
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                h16x8 bp;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) bp[j] = (h16)s[kh][8 * s2 + j];
+#pragma unroll
+                for (int t = 0; t < DH / 32; ++t) {
+                    const char *va = smem + vbo[t] + (32 * kh + 16 * s2) * RB;
+                    const h16x4 lo = lds_read_tr16(va);
+                    const h16x4 up = lds_read_tr16(va + 8 * RB);
+                    const h16x8 a = {lo[0], lo[1], lo[2], lo[3], up[0], up[1], up[2], up[3]};
+                    o[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bp, o[t], 0, 0, 0);
+                }
+            }
+        }
+    };
+    auto scores = [&](int kb, int sbase) {
+        qk(kb, sbase, true);
+        float rs = expsum();
+        if (__builtin_amdgcn_ballot_w64(rs > (float)(1 << ATT_SUMX))) {
+            qk(kb, sbase, true);
+            const float m = row_max();
+            const float sh = m > 0.f ? (float)(h16)(c + m) - c : 0.f;
+            const float alpha = __builtin_amdgcn_exp2f(-sh);
+            shift_by(sh);
+            c += sh;
+            bbias[0] = hi ? zero : (h16)(-c);
+            l *= alpha;
+#pragma unroll
+            for (int t = 0; t < DH / 32; ++t)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+            rs = expsum();
+        }
+        l += rs;
+    };
+
+#pragma unroll
+    for (int t = 0; t < DH / 32; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[t][r] = 0.f;
+    const h16 s16 = (h16)sl2;
+    const h16x8 sc = {s16, s16, s16, s16, s16, s16, s16, s16};
+    // block j: this wave's pieces of it retired (blocks j + 1 .. j + NS - 2 may
+    // fly), then the barrier publishes every wave's and frees block j - 1's stage,
+    // then block j + NS - 1 is issued into that stage
+    auto enter = [&](int j) {
+        const int younger = min(NS - 2, nblk - 1 - j);   // blocks in flight behind block j
+        if (j == 0) {   // the Q loads and block 0 (the oldest); blocks 1 .. NS - 2 may fly
+            asm volatile("s_waitcnt vmcnt(%4)" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3])
+                         : "i"(PW * (NS - 2)) : "memory");
+        } else if (younger >= 2) {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PW * 2) : "memory");
+        } else if (younger == 1) {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PW) : "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (j + NS - 1 < nblk) issue(j + NS - 1);
+    };
+    auto block0 = [&]() {                                 // lds3's block 0 (peeled)
+        qk(0, 0, false);
+        c = (float)(h16)row_max();
+        shift_by(c);
+        bbias[0] = hi ? zero : (h16)(-c);
+        l = expsum();
+        pv(0);
+    };
+    enter(0);
+#pragma unroll
+    for (int st = 0; st < DH / 16; ++st) qf[st] *= sc;
+    if (active) block0();
+#pragma clang loop unroll(disable)
+    for (int j = 1; j < nblk; ++j) {
+        enter(j);
+        if (active) {
+            const int sbase = (j % NS) * SB;
+            scores(64 * j, sbase);
+            pv(sbase);
+        }
+    }
+    // (short sentences: the clamped prologue copies may still fly; none may land
+    // after the workgroup is gone)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!active) return;
+    // lds3's store phase: 1 / l, one permlane32 swap per dword of a chunk pair,
+    // four 16-B bounds-checked stores per lane (rows >= len dropped)
+    const float inv = 1.0f / halves_sum(l);
+    const int q = q0 + 32 * w + lq;
+    uint32_t pk[DH / 8][2];
+#pragma unroll
+    for (int m = 0; m < DH / 8; ++m)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int t = m >> 2, g = m & 3;
+            const h16x2 v = {(h16)(o[t][4 * g + 2 * k] * inv), (h16)(o[t][4 * g + 2 * k + 1] * inv)};
+            pk[m][k] = __builtin_bit_cast(uint32_t, v);
+        }
+#pragma unroll
+    for (int p = 0; p < DH / 16; ++p)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const auto r = __builtin_amdgcn_permlane32_swap(pk[2 * p][k], pk[2 * p + 1][k], false, false);
+            pk[2 * p][k] = r[0];
+            pk[2 * p + 1][k] = r[1];
+        }
+    const __amdgpu_buffer_rsrc_t ors =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(out + (size_t)start * d), (short)0, len * d * 2, 0x00020000);
+    const int ob = (q * d + h * DH + 8 * hi) * 2;
+#pragma unroll
+    for (int p = 0; p < DH / 16; ++p) {
+        typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+        const u32x4v v = {pk[2 * p][0], pk[2 * p][1], pk[2 * p + 1][0], pk[2 * p + 1][1]};
+        __builtin_amdgcn_raw_buffer_store_b128(v, ors, ob + 32 * p, 0, 0);
+    }
+}
+
 thread_local int g_att_variant = 0;   // benches only (bertx_bench_attention), per calling thread
 
 // BERT_ATT_SHORT=0: short batches through attention_lds3 as well (A/B)
@@ -865,6 +1142,16 @@ void launch_attention(const uint16_t *qkv, const int32_t *cu, int32_t n_seqs, in
             if (max_len <= 64 && g_att_variant != 7 && g_att_variant != 8 && att_short_env()) {
                 if (n_items > 0)
                     attention_short_kernel<<<n_items, 128, 0, s>>>((const h16 *)qkv, cu, d, n_head, sl2, (h16 *)out);
+                return;
+            }
+            // 64 < max_len <= 512: attention_pp (two 8-wave workgroups per CU, half an
+            // item each: 66.2-67.1 vs lds3 67.5-68.2 us at C3, the same bits,
+            // profiles/r06_attention_pp_ab.log); variant 7 / 8 or BERT_ATT_PP=0 run
+            // attention_lds3 (tests, A/B)
+            static const bool pp_env = [] { const char *e = std::getenv("BERT_ATT_PP"); return !(e && *e == '0'); }();
+            if (g_att_variant != 7 && g_att_variant != 8 && pp_env) {
+                if (n_items > 0)
+                    attention_pp_kernel<<<2 * n_items, 512, 0, s>>>((const h16 *)qkv, cu, d, n_head, sl2, (h16 *)out);
                 return;
             }
             const int cap = g_att_variant == 7 ? 7 : device_cu_count();

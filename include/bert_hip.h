@@ -163,8 +163,10 @@ BERT_API int32_t bertx_bench_gemm(int32_t fmt, int32_t N, int32_t K, int32_t M, 
 /*
  * Attention micro-benchmark on random operands (device 0): average device time
  * of `iters` launches for n_seqs sentences of `len` tokens, n_head heads of size
- * dh; variant 0 = the production kernel, 7 = the same on at most 7 workgroups
- * (many ragged items per workgroup).
+ * dh; variant 0 = the production kernels (attention_pp for 64 < L <= 512 at dh
+ * 64, attention_short for L <= 64), 8 = attention_lds3 (the persistent 16-wave
+ * kernel, bitwise the same), 7 = lds3 on at most 7 workgroups (many ragged items
+ * per workgroup).
  */
 BERT_API int32_t bertx_bench_attention(int32_t n_seqs, int32_t len, int32_t n_head, int32_t dh, int32_t variant,
                                        int32_t iters, float *avg_us);

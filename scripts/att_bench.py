@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Attention micro-benchmark: production kernel (0) and its 7-workgroup form (7)."""
+"""Attention micro-benchmark: the production kernels (0: attention_pp for 64 < L <=
+512, dh 64), attention_lds3 (8) and its 7-workgroup form (7); VARIANTS picks them."""
 import ctypes
 import os
 import sys
@@ -9,7 +10,7 @@ sys.path.insert(0, os.path.join(ROOT, "embeddings.cpp_amd"))
 import bertpy  # noqa: E402
 
 L = bertpy.load_lib()
-variants = [int(v) for v in os.environ.get("VARIANTS", "0,7").split(",")]
+variants = [int(v) for v in os.environ.get("VARIANTS", "0,8").split(",")]
 for rnd in range(int(os.environ.get("ROUNDS", "3"))):
     for n_seqs, ln, nh, dh in [(64, 512, 12, 64), (32, 128, 12, 32)]:
         for v in variants:

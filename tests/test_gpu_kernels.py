@@ -359,7 +359,7 @@ def attention_ref(qkv, cu, n_head, d):
     return out
 
 
-@pytest.mark.parametrize("variant,dh", [(0, 64), (7, 64), (-1, 64), (0, 32), (-1, 32)])
+@pytest.mark.parametrize("variant,dh", [(0, 64), (8, 64), (7, 64), (-1, 64), (0, 32), (-1, 32)])
 def test_attention_matches_numpy(lib, variant, dh):
     """Ragged sentences (1 .. 512 tokens, block edges), one with sharp scores whose row
     maximum moves late (exercises the production kernel's offset move + rescale).
@@ -412,6 +412,35 @@ def test_short_attention_bitwise_equal_to_lds3(lib, seed):
     got = outs[0].astype(np.float64)
     assert np.isfinite(got).all()
     assert np.abs(got - ref).max() < 6e-3 * max(1.0, np.abs(ref).max())
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_attention_pp_bitwise_equal_to_lds3(lib, seed):
+    """attention_pp (the production kernel for 64 < L <= 512: two 8-wave
+    workgroups per CU, half an item's queries each, K/V streamed through a
+    4-stage ring of 64-key blocks) runs lds3's per-query block sequence on the
+    same wave composition: bitwise equal to attention_lds3 (variant 8) on ragged
+    lengths around every block, half-item and ring boundary, and within tolerance
+    of numpy; seed 2 scales the scores so the offset-moving rescale path runs."""
+    n_head, dh = 12, 64
+    d = n_head * dh
+    lens = [1, 63, 64, 65, 128, 191, 192, 255, 256, 257, 300, 383, 448, 511, 512, 17]
+    cu = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    T = int(cu[-1])
+    rng = np.random.default_rng(seed)
+    qkv = (rng.standard_normal((T, 3 * d)) * (1.0 + 3.0 * seed)).astype(np.float16)
+    outs = {}
+    for variant in (0, 8):
+        out = np.zeros((T, d), np.float16)
+        rc = lib.bertx_test_attention(qkv.ctypes.data, cu.ctypes.data, len(lens), n_head, d, variant, out.ctypes.data)
+        assert rc == 0
+        outs[variant] = out
+    assert np.array_equal(outs[0].view(np.uint16), outs[8].view(np.uint16))
+    got = outs[0].astype(np.float64)
+    assert np.isfinite(got).all()
+    if seed < 2:   # (seed 2's peaked scores: lds3's own f16 P bounds its error; the bits are the check)
+        ref = attention_ref(qkv, cu, n_head, d)
+        assert np.abs(got - ref).max() < 6e-3 * max(1.0, np.abs(ref).max())
 
 
 @pytest.mark.parametrize("fmt", [1, 2, 3, 8])
