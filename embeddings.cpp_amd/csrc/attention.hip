@@ -857,7 +857,8 @@ __global__ __launch_bounds__(128) void attention_short_kernel(const h16 *__restr
 // wave composition, so the output has lds3's bits (the kernel tests compare them).
 // (Round 6 also measured, all bitwise equal and slower: four 4-wave workgroups
 // per CU with a 2-stage ring, a barrier per block pair, and a persistent form
-// whose ring runs on across units; profiles/r06_attention_pp_ab.log.)
+// whose ring runs on across units; profiles/r06_attention_pp_ab.log.  A priority
+// split between the co-resident workgroups: no effect, r06_attention_pp_prio_ab.log.)
 __global__ __launch_bounds__(512, 4) void attention_pp_kernel(const h16 *__restrict__ qkv,
                                                               const int32_t *__restrict__ cu, int d, int nh,
                                                               float sl2, h16 *__restrict__ out)

@@ -11,6 +11,7 @@ import glob
 import os
 import re
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -44,6 +45,17 @@ def test_exports_every_declared_symbol(lib):
     assert names <= exported, names - exported
     # nothing but the ABI leaks out (hidden visibility for everything else)
     assert {n for n in exported if not n.startswith(("bert", "ggml_"))} <= {"_init", "_fini"}
+
+
+@pytest.mark.parametrize("checker", ["check_drain.py", "check_asm_loads.py"])
+def test_code_object_checks(lib, checker):
+    """The shipped gfx950 code objects, disassembled: every GEMM / attention kernel
+    drains its hand-counted asm LDS reads before the epilogue (check_drain, round 3's
+    fault class), and attention_pp touches no Q register while its asm Q loads are
+    in flight (check_asm_loads)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", checker),
+                        os.path.join(ROOT, "build", "libbert.so")], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
 
 
 def test_version_and_time(lib):
