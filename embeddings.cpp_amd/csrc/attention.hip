@@ -880,6 +880,8 @@ __global__ __launch_bounds__(512, 4) void attention_pp_kernel(const h16 *__restr
     const int nblk = (len + 63) >> 6;
     const bool active = q0 + 32 * w < len;                // wave-uniform
     const h16 *kbase = qkv + (size_t)start * ld + d + h * DH;
+    PST_DECL;   // (stamps builds only, diag_att_stamps.h)
+    PST_SET(0, PST_NOW());
 
     // block j's K and V rows into stage j % NS: piece i < 8 is K rows 8i .. 8i + 7
     // of the block, 8 + i the same V rows (K swizzled by (row >> 1) & 7, V by
@@ -1070,18 +1072,26 @@ __global__ __launch_bounds__(512, 4) void attention_pp_kernel(const h16 *__restr
         pv(0);
     };
     enter(0);
+    PST_SET(1, PST_NOW());
 #pragma unroll
     for (int st = 0; st < DH / 16; ++st) qf[st] *= sc;
     if (active) block0();
+    PST_SET(2, PST_NOW());
 #pragma clang loop unroll(disable)
     for (int j = 1; j < nblk; ++j) {
+        PST_MARK();
         enter(j);
+        PST_ADDW();
+        PST_MARK();
         if (active) {
             const int sbase = (j % NS) * SB;
             scores(64 * j, sbase);
             pv(sbase);
         }
+        PST_ADDC();
     }
+    PST_SUMS();
+    PST_SET(5, PST_NOW());
     // (short sentences: the clamped prologue copies may still fly; none may land
     // after the workgroup is gone)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1116,6 +1126,8 @@ __global__ __launch_bounds__(512, 4) void attention_pp_kernel(const h16 *__restr
         const u32x4v v = {pk[2 * p][0], pk[2 * p][1], pk[2 * p + 1][0], pk[2 * p + 1][1]};
         __builtin_amdgcn_raw_buffer_store_b128(v, ors, ob + 32 * p, 0, 0);
     }
+    PST_SET(6, PST_NOW());
+    PST_HWID();
 }
 
 thread_local int g_att_variant = 0;   // benches only (bertx_bench_attention), per calling thread

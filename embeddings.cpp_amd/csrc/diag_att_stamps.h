@@ -43,4 +43,30 @@ extern "C" __attribute__((visibility("default"))) int bertx_att_stamps(unsigned 
 #define ASTAMP_ITEM_END(nit) do { } while (0)
 #endif
 
+// ---------------------------------------------------------------------------
+// attention_pp: per workgroup (unit) and wave, slots 0 unit start, 1 after block
+// 0's wait + barrier, 2 after block 0, 3 / 4 cycles summed over blocks >= 1 in
+// the wait + barrier + issue / in the block's compute, 5 after the block loop,
+// 6 after the stores, 7 HW_ID.  PST_* need `lane` and `w` in scope.
+// ---------------------------------------------------------------------------
+#ifdef ATT_STAMPS
+#define PST_DECL unsigned long long pst_t = 0, pst_w = 0, pst_c = 0
+#define PST_SET(k, v) do { if (lane == 0) g_att_stamps[((size_t)blockIdx.x * 8 + w) * 8 + (k)] = (v); } while (0)
+#define PST_NOW() __builtin_amdgcn_s_memtime()
+#define PST_MARK() (pst_t = __builtin_amdgcn_s_memtime())
+#define PST_ADDW() (pst_w += __builtin_amdgcn_s_memtime() - pst_t)
+#define PST_ADDC() (pst_c += __builtin_amdgcn_s_memtime() - pst_t)
+#define PST_SUMS() do { PST_SET(3, pst_w); PST_SET(4, pst_c); } while (0)
+#define PST_HWID() PST_SET(7, (unsigned long long)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11)))
+#else
+#define PST_DECL do { } while (0)
+#define PST_SET(k, v) do { } while (0)
+#define PST_NOW() 0
+#define PST_MARK() do { } while (0)
+#define PST_ADDW() do { } while (0)
+#define PST_ADDC() do { } while (0)
+#define PST_SUMS() do { } while (0)
+#define PST_HWID() do { } while (0)
+#endif
+
 }  // namespace emb
