@@ -58,6 +58,23 @@ def test_code_object_checks(lib, checker):
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
 
 
+def test_asm_load_checker_catches_the_hazard():
+    """check_asm_loads' rule on hand-written sequences: the hipcc copy that round 6
+    met (a v_mov of a pending Q register in front of the tied wait) and an address
+    taken from a pending destination are caught; the shipped shape passes."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import check_asm_loads as c
+    loads = ["global_load_dwordx4 v[14:17], v[2:3], off", "v_lshl_add_u64 v[4:5], v[2:3], 0, 32",
+             "global_load_dwordx4 v[10:13], v[4:5], off", "global_load_dwordx4 v[6:9], v[4:5], off",
+             "global_load_dwordx4 v[2:5], v[2:3], off"]
+    wait = ["s_waitcnt vmcnt(4)"]
+    assert c.check(loads + ["v_mov_b32_e32 v20, s1"] + wait) is None
+    assert c.check(loads + ["v_mov_b64_e32 v[32:33], v[14:15]"] + wait) is not None
+    bad_addr = ["global_load_dwordx4 v[14:17], v[2:3], off", "global_load_dwordx4 v[10:13], v[14:15], off",
+                "global_load_dwordx4 v[6:9], v[4:5], off", "global_load_dwordx4 v[2:5], v[4:5], off"]
+    assert c.check(bad_addr + wait) is not None
+
+
 def test_version_and_time(lib):
     v = lib.bertx_version().decode()
     assert "gfx950" in v
