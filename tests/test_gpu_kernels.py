@@ -443,6 +443,32 @@ def test_attention_pp_bitwise_equal_to_lds3(lib, seed):
         assert np.abs(got - ref).max() < 6e-3 * max(1.0, np.abs(ref).max())
 
 
+def test_attention_pp_bitwise_stress(lib):
+    """attention_pp's Q rows arrive by asm loads retired by one tied wait, and its
+    K/V by a ring of LDS-DMA pieces with counted waits: a missed wait would show as
+    a timing-dependent difference.  24 random ragged batches (1-64 sentences of
+    1-512 tokens, 12 heads), each bitwise equal to attention_lds3."""
+    n_head, dh = 12, 64
+    d = n_head * dh
+    rng = np.random.default_rng(77)
+    for it in range(24):
+        n = int(rng.integers(1, 65))
+        lens = rng.integers(65, 513, n) if it % 3 else rng.integers(1, 513, n)
+        lens[0] = 512 if it % 4 == 0 else lens[0]
+        if max(lens) <= 64:
+            lens[0] = 65
+        cu = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+        T = int(cu[-1])
+        qkv = (rng.standard_normal((T, 3 * d)) * 1.5).astype(np.float16)
+        outs = []
+        for variant in (0, 8):
+            out = np.zeros((T, d), np.float16)
+            assert lib.bertx_test_attention(qkv.ctypes.data, cu.ctypes.data, n, n_head, d, variant,
+                                            out.ctypes.data) == 0
+            outs.append(out)
+        assert np.array_equal(outs[0].view(np.uint16), outs[1].view(np.uint16)), (it, list(lens[:8]))
+
+
 @pytest.mark.parametrize("fmt", [1, 2, 3, 8])
 @pytest.mark.parametrize("cfg", [2, 3, 11, 16])
 def test_small_tiles_bitwise_equal_to_64x64(lib, fmt, cfg):
