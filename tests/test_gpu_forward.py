@@ -138,6 +138,29 @@ def test_fake_batch_and_forward(quant_models):
     assert np.all(cosines(one[None], o.forward_batch(ids[1:2])) >= 1 - COS_TOL)
 
 
+def test_empty_and_degenerate_batches(quant_models):
+    """Edge cases of the ABI on a device: an empty batch (forward and encode) is a
+    no-op; an empty text encodes as [CLS] [SEP] and a one-token sentence runs, both
+    unit-norm and within the cosine bound of the oracle; a sentence at exactly
+    n_max_tokens runs beside a one-token one, each bitwise as it is alone."""
+    path = quant_models[("tiny64", "q4_0")]
+    m = bertpy.BertModel(path)
+    o = oracle_lib.Oracle(path)
+    assert m.forward_batch([]).shape == (0, m.n_embd)
+    assert m.encode([]).shape == (0, m.n_embd)
+    e = m.encode(["", "a"], batch_size=2)
+    assert np.all(np.isfinite(e)) and np.allclose(np.linalg.norm(e, axis=1), 1.0, atol=1e-5)
+    ref, written = o.encode_batch(["", "a"], 2)
+    assert written.all()
+    assert np.all(cosines(e, ref) >= 1 - COS_TOL)
+    ids = ragged_ids(690, [1, m.n_max_tokens], seed=9)
+    both = m.forward_batch(ids)
+    assert np.all(np.isfinite(both))
+    assert np.all(cosines(both, o.forward_batch(ids)) >= 1 - COS_TOL)
+    for i in range(2):
+        assert np.array_equal(m.forward_batch([ids[i]])[0], both[i])
+
+
 def test_too_long_is_refused(quant_models):
     m = bertpy.BertModel(quant_models[("tiny32", "f16")])
     ids = ragged_ids(690, [10, 129])          # n_max_tokens = 128
