@@ -787,7 +787,10 @@ int pick_cfg(int N, int M, int cfg)
     if (cfg == 0) {
         // the largest tile that still gives every CU work: 256 x 128 tiles two per CU
         // (measured fastest at C3 once there are two per CU, profiles/r01_gemm16_sweep.log),
-        // else 128 x 128 once there is one per CU, else 64 x 64 (small batches)
+        // else 128 x 128 once they cover half the CUs (one such tile per CU beats the
+        // 64 x 64 tiles that would spread over all of them: MiniLM QKV at M 2,048 7.3 vs
+        // 8.6 us, bge-base FFN-up at M 1,024 11.2 vs 14.7 us, profiles/r06_cfg34_crossover.log),
+        // else 64 x 64 (small batches)
         const long n128 = (N + 127) / 128, cus = device_cu_count();
         // small batches: 64-row tiles; while they fill less than half the CUs, on 4
         // waves (2 along the tokens: every SIMD of a CU works, each wave's K-step
@@ -797,7 +800,7 @@ int pick_cfg(int N, int M, int cfg)
         // there).  Same bits either way.
         const long n64 = (long)(M / 64) * ((N + 63) / 64);
         const int small = 2 * n64 < cus ? 16 : 4;
-        cfg = (M % 256 == 0 && (M / 256) * n128 >= 2 * cus) ? 2 : (M % 128 == 0 && (M / 128) * n128 >= cus) ? 3 : small;
+        cfg = (M % 256 == 0 && (M / 256) * n128 >= 2 * cus) ? 2 : (M % 128 == 0 && 2 * (M / 128) * n128 >= cus) ? 3 : small;
     }
     if ((cfg == 2 || cfg == 11) && M % 256) cfg = 3;
     if (cfg == 3 && M % 128) cfg = 4;
@@ -805,10 +808,16 @@ int pick_cfg(int N, int M, int cfg)
     return cfg;
 }
 
-// Statistics-fold capacity (LnFold::in_part) of a config: the partial groups its
-// LDS holds (cfg 3 keeps two workgroups per CU with 12: d <= 384; the 64-row
-// forms with 24: d <= 768); 0 = no fold form (the 256-row large-batch tiles).
-constexpr int fold_cap(int cfg) { return cfg == 3 ? 12 : (cfg == 4 || cfg == 16) ? 24 : 0; }
+// Statistics-fold capacity (LnFold::in_part) of a config for N features over M
+// rows: the partial groups its LDS holds (cfg 3 keeps two workgroups per CU with
+// 12: d <= 384, and holds 24 on one workgroup per CU where its tiles are at most
+// one per CU; the 64-row forms 24: d <= 768); 0 = no fold form (the 256-row
+// large-batch tiles).
+int fold_cap(int cfg, int N, int M)
+{
+    if (cfg == 3) return (long)(M / 128) * ((N + 127) / 128) <= device_cu_count() ? 24 : 12;
+    return (cfg == 4 || cfg == 16) ? 24 : 0;
+}
 
 template <int FMT>
 int launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, int32_t epi, const void *res,
@@ -818,10 +827,15 @@ int launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, i
     if (ln.in_part) {
         // statistics fold: the caller made sure the config has the capacity
         // (gemm_fold_ok); anything else is an error, never a silent fallback
-        if (!lnf || epi == EPI_BIAS_RES || ln.in_G <= 0 || ln.in_G > fold_cap(cfg) || 32 * ln.in_G != (W.kx ? W.kx : W.K))
+        if (!lnf || epi == EPI_BIAS_RES || ln.in_G <= 0 || ln.in_G > fold_cap(cfg, W.N, M) ||
+            32 * ln.in_G != (W.kx ? W.kx : W.K))
             return -1;
         switch (cfg) {
-        case 3: dispatch_z<FMT, 4, 128, 4, 1, 3, 1, 0, 2, 12>(W, x, M, bias, epi, res, out, s, ln, lnf); break;
+        case 3:
+            // (the 24-group form: 91 KiB of LDS, one workgroup per CU)
+            if (ln.in_G <= 12) dispatch_z<FMT, 4, 128, 4, 1, 3, 1, 0, 2, 12>(W, x, M, bias, epi, res, out, s, ln, lnf);
+            else dispatch_z<FMT, 4, 128, 4, 1, 3, 1, 0, 1, 24>(W, x, M, bias, epi, res, out, s, ln, lnf);
+            break;
         case 16: dispatch_z<FMT, 4, 64, 4, 1, 3, 2, 3, 2, 24>(W, x, M, bias, epi, res, out, s, ln, lnf); break;
         default: dispatch_z<FMT, 2, 64, 4, 1, 3, 1, 0, 2, 24>(W, x, M, bias, epi, res, out, s, ln, lnf); break;
         }
@@ -855,7 +869,8 @@ static int forward_cfg()
 
 bool gemm_fold_ok(const DevWeight &W, int32_t M, int32_t G)
 {
-    return G > 0 && M > 0 && M % 64 == 0 && 32 * G == (W.kx ? W.kx : W.K) && G <= fold_cap(pick_cfg(W.N, M, forward_cfg()));
+    return G > 0 && M > 0 && M % 64 == 0 && 32 * G == (W.kx ? W.kx : W.K) &&
+           G <= fold_cap(pick_cfg(W.N, M, forward_cfg()), W.N, M);
 }
 
 // CUs of the calling thread's current device, cached per ordinal (a context may

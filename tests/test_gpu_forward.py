@@ -564,6 +564,26 @@ def test_short_sentences_bitwise_across_tile_forms(tmp_path, ftype):
     assert np.array_equal(m.forward_batch(short), full[:3])
 
 
+@pytest.mark.parametrize("arch,ftype,n", [("all-MiniLM-L6-v2", "f16", 16), ("bge-base-en-v1.5", "q4_0", 8)])
+def test_mid_batch_tile_forms_bitwise(tmp_path, arch, ftype, n):
+    """Mid-size batches (1-2k GEMM rows) take 128 x 128 tiles once those cover half the
+    CUs (gemm.hip pick_cfg), with the statistics fold in its one-workgroup-per-CU
+    24-group form at d 768: every sentence keeps the bits it has alone (64-row tile
+    forms) and in a pair, and the batch is within the cosine bound of the oracle."""
+    hp = bertpy.ARCHS[arch]
+    path = str(tmp_path / f"{arch}-{ftype}.bin")
+    bertpy.synthetic_model(path, arch, ftype, seed=1234)
+    m = bertpy.BertModel(path)
+    ids = ragged_ids(hp["n_vocab"], [128] * n, seed=12)
+    full = m.forward_batch(ids)
+    assert np.all(np.isfinite(full))
+    for i in (0, n // 2, n - 1):
+        assert np.array_equal(m.forward_batch([ids[i]])[0], full[i]), (arch, i)
+    assert np.array_equal(m.forward_batch(ids[:2]), full[:2])
+    ref = oracle_lib.Oracle(path).forward_batch(ids[:2], n_threads=min(16, os.cpu_count() or 1))
+    assert np.all(cosines(full[:2], ref) >= 1 - COS_TOL)
+
+
 def test_load_free_cycles_multi_replica(quant_models, monkeypatch):
     """The load path that aborted on round 5's driver box, exercised repeatedly: ten
     cycles of a 4-replica context on one GPU (load, a small forward on the routed

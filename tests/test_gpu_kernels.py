@@ -260,14 +260,16 @@ def ln_row_stats_f32(part, d):
 @pytest.mark.parametrize("fmt", [1, 2, 3, 8])
 @pytest.mark.parametrize("epi", [0, 1])
 @pytest.mark.parametrize("N,K,M,cfg", [(1152, 384, 4096, 0), (1536, 384, 200, 3), (2304, 768, 32, 0),
-                                       (3072, 768, 64, 16), (768, 768, 1000, 4), (192, 64, 10, 0)])
+                                       (3072, 768, 64, 16), (768, 768, 1000, 4), (192, 64, 10, 0),
+                                       (2304, 768, 1024, 3), (3072, 768, 1024, 0)])
 def test_gemm_statistics_fold(lib, fmt, epi, N, K, M, cfg):
     """The statistics fold of the small-batch forward (LnFold::in_part): the GEMM
     combines the residual GEMM's per-group partials itself.  Its statistics are
     bitwise the statistics kernel's (ln_stats, the launch form) and within rounding
     of ln_row_stats restated in numpy float32, and its output is bitwise the output
     of the same GEMM given those statistics, for every fold config (3: 128-row
-    tiles up to d 384; 4, 16: 64-row tiles up to d 768)."""
+    tiles up to d 384, and up to d 768 where they are at most one per CU -- the
+    one-workgroup-per-CU form; 4, 16: 64-row tiles up to d 768)."""
     rng = np.random.default_rng(fmt * 5 + epi + N + M)
     W = rng.standard_normal((N, K)).astype(np.float32) * 0.05
     wb, deq = weight_rows(fmt, W)
