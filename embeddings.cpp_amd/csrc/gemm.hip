@@ -782,7 +782,7 @@ void dispatch_z(const DevWeight &W, const h16 *x, int M, const float *bias, int 
 // A config whose row tile does not divide M falls back to the next smaller tile.
 // The tile config a launch of N features over M rows runs (cfg 0: the heuristic),
 // after the fallbacks for tiles that do not divide M.
-int pick_cfg(int N, int M, int cfg)
+int pick_cfg(int N, int M, int cfg, int fmt)
 {
     if (cfg == 0) {
         // the largest tile that still gives every CU work: 256 x 128 tiles two per CU
@@ -792,14 +792,15 @@ int pick_cfg(int N, int M, int cfg)
         // 8.6 us, bge-base FFN-up at M 1,024 11.2 vs 14.7 us, profiles/r06_cfg34_crossover.log),
         // else 64 x 64 (small batches)
         const long n128 = (N + 127) / 128, cus = device_cu_count();
-        // small batches: 64-row tiles; while they fill less than half the CUs, on 4
-        // waves (2 along the tokens: every SIMD of a CU works, each wave's K-step
+        // small batches: 64-row tiles.  Quantized weights on 4 waves (2 along the
+        // tokens: every SIMD of a CU works, each wave's K-step and dequantization
         // half as long; B = 1, L = 32: 632 -> 571 us) with wave-private X rings (no
-        // barrier in the K loop: 582 -> 567 us, profiles/r03_gemm_private_ab.log),
-        // else on 2 (C2's O-proj and FFN-down: the 4-wave forms 6-15 % slower
-        // there).  Same bits either way.
-        const long n64 = (long)(M / 64) * ((N + 63) / 64);
-        const int small = 2 * n64 < cus ? 16 : 4;
+        // barrier in the K loop: 582 -> 567 us, profiles/r03_gemm_private_ab.log) --
+        // round 6: at every M up to the 128 x 128 threshold, not only below half the
+        // CUs (bge-base FFN-down at M 1,024 16.8 vs 20.9 us); f16 weights (nothing
+        // to dequantize, four weight loads per K-step) on 2 waves, 0.5-2 us faster
+        // at every width and M (profiles/r06_cfg_small_sweep.log).  Same bits either way.
+        const int small = fmt == FMT_F16 ? 4 : 16;
         cfg = (M % 256 == 0 && (M / 256) * n128 >= 2 * cus) ? 2 : (M % 128 == 0 && 2 * (M / 128) * n128 >= cus) ? 3 : small;
     }
     if ((cfg == 2 || cfg == 11) && M % 256) cfg = 3;
@@ -823,7 +824,7 @@ template <int FMT>
 int launch_fmt(const DevWeight &W, const h16 *x, int32_t M, const float *bias, int32_t epi, const void *res,
                void *out, hipStream_t s, LnFold ln, bool lnf, int cfg)
 {
-    cfg = pick_cfg(W.N, M, cfg);
+    cfg = pick_cfg(W.N, M, cfg, FMT);
     if (ln.in_part) {
         // statistics fold: the caller made sure the config has the capacity
         // (gemm_fold_ok); anything else is an error, never a silent fallback
@@ -870,7 +871,7 @@ static int forward_cfg()
 bool gemm_fold_ok(const DevWeight &W, int32_t M, int32_t G)
 {
     return G > 0 && M > 0 && M % 64 == 0 && 32 * G == (W.kx ? W.kx : W.K) &&
-           G <= fold_cap(pick_cfg(W.N, M, forward_cfg()), W.N, M);
+           G <= fold_cap(pick_cfg(W.N, M, forward_cfg(), W.fmt), W.N, M);
 }
 
 // CUs of the calling thread's current device, cached per ordinal (a context may

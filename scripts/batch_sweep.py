@@ -16,9 +16,10 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 import bertpy  # noqa: E402
 
-CASES = [("all-MiniLM-L6-v2", "f16", 128, [int(x) for x in os.environ.get("SWEEP_MINILM", "8,12,16,20,24,28,32").split(",")]),
-         ("bge-base-en-v1.5", "q4_0", 512, [int(x) for x in os.environ.get("SWEEP_BGE512", "1,2,3,4,6,8").split(",")]),
-         ("bge-base-en-v1.5", "q4_0", 128, [int(x) for x in os.environ.get("SWEEP_BGE128", "8,16,24,32").split(",")])]
+# SWEEP_CASES: "arch:ftype:L:B,B,...;..." (default: the round-6 mid-batch sweep)
+SPEC = os.environ.get("SWEEP_CASES", "all-MiniLM-L6-v2:f16:128:8,12,16,20,24,28,32;"
+                      "bge-base-en-v1.5:q4_0:512:1,2,3,4,6,8;bge-base-en-v1.5:q4_0:128:8,16,24,32")
+CASES = [(a, f, int(L), [int(x) for x in bs.split(",")]) for a, f, L, bs in (c.split(":") for c in SPEC.split(";") if c)]
 model_dir = os.environ.get("SWEEP_MODEL_DIR", "/tmp/bench_models")
 steps = int(os.environ.get("SWEEP_STEPS", "50"))
 lib = bertpy.load_lib()
