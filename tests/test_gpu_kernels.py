@@ -471,6 +471,22 @@ def test_attention_pp_bitwise_stress(lib):
         assert np.array_equal(outs[0].view(np.uint16), outs[1].view(np.uint16)), (it, list(lens[:8]))
 
 
+@pytest.mark.parametrize("fmt,N,K,M,want", [
+    (1, 384, 1536, 256, 4), (1, 1152, 384, 1024, 4), (2, 768, 3072, 1024, 16), (8, 2304, 768, 512, 16),
+    (3, 1024, 4096, 1024, 16), (2, 2304, 768, 1024, 3), (1, 1152, 384, 2048, 3), (1, 1536, 384, 4096, 3),
+    (2, 3072, 768, 32768, 2), (8, 768, 3072, 32768, 2)])
+def test_gemm_tile_heuristic(lib, fmt, N, K, M, want):
+    """The tile form the heuristic (gemm.hip pick_cfg, cfg 0) runs on a 256-CU MI355X,
+    pinned so a change to it is deliberate: 64 x 64 tiles for small M -- 2 waves for
+    f16 weights, 4 waves with wave-private X rings for q4_0 / q4_1 / q8_0
+    (profiles/r06_cfg_small_sweep.log, r06_cfg_small_q41.log) -- 128 x 128 once those
+    cover half the CUs (r06_cfg34_crossover.log), 256 x 128 at two per CU."""
+    # (the choices assume the 256 CUs of one MI355X in SPX mode, as on the test boxes)
+    us = ctypes.c_float()
+    assert lib.bertx_bench_gemm(fmt, N, K, M, 0 if N > K else 2, 0, 1, ctypes.byref(us)) == 0
+    assert lib.bertx_test_gemm_ran() == want
+
+
 @pytest.mark.parametrize("fmt", [1, 2, 3, 8])
 @pytest.mark.parametrize("cfg", [2, 3, 11, 16])
 def test_small_tiles_bitwise_equal_to_64x64(lib, fmt, cfg):
